@@ -1,0 +1,98 @@
+/*
+ * unsamflow_hip.h — C ABI of libunsamflow_hip.so, the MI355X (gfx950) native
+ * plugin behind UnSAMFlow's cost-volume hot path.
+ *
+ * This library replaces, for the PWCLite call sites, the reference's native
+ * plugin and the ATen sampler it leans on:
+ *
+ *   usf_corr_fwd_f32  <- correlation_cuda.forward
+ *                        (models/correlation_package/correlation_cuda.cc:10-86,
+ *                         pybind export :167-170; Python caller
+ *                         models/correlation_package/correlation.py:9-38)
+ *   usf_corr_bwd_f32  <- correlation_cuda.backward
+ *                        (models/correlation_package/correlation_cuda.cc:88-165;
+ *                         Python caller correlation.py:40-72)
+ *   usf_warp_fwd_f32  <- grid_sample(bilinear, align_corners=True) inside
+ *                        flow_warp (utils/warp_utils.py:97-106, incl.
+ *                        mesh_grid :7-13 and norm_grid :16-23)
+ *   usf_warp_bwd_f32  <- grid_sampler_2d_backward reached from flow_warp's
+ *                        autograd graph (warp_utils.py:103-105)
+ *
+ * Contract (all entry points):
+ *   - Pointers are DEVICE pointers to fp32 NCHW tensors. x/x1/x2/gout/out/gx*
+ *     are dense (contiguous). The flow tensor may have any batch stride
+ *     (flow_bstride, in elements) with a dense [2,H,W] per-sample block, so
+ *     the loss's channel slices flow[:, :2] / flow[:, 2:]
+ *     (losses/flow_loss.py:130-131) need no copy.
+ *   - The caller allocates every output; the library never allocates,
+ *     never keeps a pointer after return and has no global state except a
+ *     thread-local error string. Calls are reentrant (the backward runs on the
+ *     autograd engine's device thread).
+ *   - Calls are asynchronous on `stream` (a hipStream_t; NULL = legacy
+ *     default stream).
+ *   - Return value: 0 on success; a positive hipError_t from a failed
+ *     launch; USF_EINVAL (-1) for bad arguments (nothing launched).
+ *     usf_last_error_string() describes the last failure on this thread.
+ *     The reference instead returned 1/0 and raised AT_ERROR("CUDA call
+ *     failed") (correlation_cuda.cc:80-82, :160-162); the Python layer raises
+ *     RuntimeError with this string.
+ *   - Nullable gradient outputs mean "not needed" (ctx.needs_input_grad).
+ */
+#ifndef UNSAMFLOW_HIP_H
+#define UNSAMFLOW_HIP_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define USF_ABI_VERSION 1
+#define USF_EINVAL (-1)
+
+/* padding modes for the warp (flow_warp `pad` argument) */
+#define USF_PAD_ZEROS 0
+#define USF_PAD_BORDER 1
+
+/* ABI version of the loaded library (== USF_ABI_VERSION it was built with). */
+int usf_abi_version(void);
+
+/* Human-readable description of the last error on the calling thread
+ * ("" if none). The pointer stays valid until the next call on this thread. */
+const char* usf_last_error_string(void);
+
+/* Local correlation, forward.
+ *   out[b, (dy+d)*(2d+1)+(dx+d), y, x] =
+ *       (1/C) * sum_c x1[b,c,y,x] * X2(b,c,y+dy,x+dx),  X2 = 0 outside HxW
+ * x1, x2: [B,C,H,W]; out: [B,(2d+1)^2,H,W]. 1 <= d <= 4.
+ * Semantics of correlation_native.py:13-23 == correlation_cuda forward with
+ * pad_size=d, kernel_size=1, stride1=stride2=1 (correlation_cuda.cc:19-34). */
+int usf_corr_fwd_f32(const float* x1, const float* x2, float* out,
+                     int B, int C, int H, int W, int d, void* stream);
+
+/* Local correlation, backward. gout: [B,(2d+1)^2,H,W].
+ *   gx1[b,c,y,x] = (1/C) sum_k gout[b,k,y,x]       * X2(b,c,y+dy_k,x+dx_k)
+ *   gx2[b,c,y,x] = (1/C) sum_k G(b,k,y-dy_k,x-dx_k) * X1(b,c,y-dy_k,x-dx_k)
+ * gx1 / gx2 may be NULL (not needed). Outputs are overwritten (not
+ * accumulated) and the result is deterministic (no atomics). */
+int usf_corr_bwd_f32(const float* x1, const float* x2, const float* gout,
+                     float* gx1, float* gx2,
+                     int B, int C, int H, int W, int d, void* stream);
+
+/* Bilinear backward warp (flow_warp), align_corners=True.
+ * x: [B,C,H,W]; flow: [B,2,H,W] with batch stride flow_bstride (elements);
+ * out: [B,C,H,W]. pad_mode: USF_PAD_BORDER or USF_PAD_ZEROS. */
+int usf_warp_fwd_f32(const float* x, const float* flow, long long flow_bstride,
+                     float* out, int B, int C, int H, int W, int pad_mode,
+                     void* stream);
+
+/* Backward of usf_warp_fwd_f32. gout: [B,C,H,W] dense.
+ * gx: [B,C,H,W] or NULL; it is ACCUMULATED into (fp32 atomics) and must be
+ *     zeroed by the caller; summation order is not deterministic.
+ * gflow: [B,2,H,W] dense or NULL; overwritten, deterministic. */
+int usf_warp_bwd_f32(const float* x, const float* flow, long long flow_bstride,
+                     const float* gout, float* gx, float* gflow,
+                     int B, int C, int H, int W, int pad_mode, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* UNSAMFLOW_HIP_H */

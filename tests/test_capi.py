@@ -1,0 +1,103 @@
+"""C-ABI boundary checks that need no GPU: the library loads, exports exactly
+what include/unsamflow_hip.h declares, reports its ABI version, and rejects bad
+arguments with USF_EINVAL + an error string before touching the device."""
+import ctypes
+import re
+import subprocess
+
+import pytest
+
+from conftest import REPO
+
+HEADER = REPO / "include" / "unsamflow_hip.h"
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from unsamflow_amd import _lib
+    from unsamflow_amd.build import build_library
+
+    build_library()
+    return _lib.load()
+
+
+def declared_symbols():
+    text = HEADER.read_text()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(usf_\w+)\s*\(", text)))
+
+
+def test_header_declares_the_abi():
+    syms = declared_symbols()
+    assert syms == sorted(
+        ["usf_abi_version", "usf_last_error_string", "usf_corr_fwd_f32", "usf_corr_bwd_f32",
+         "usf_warp_fwd_f32", "usf_warp_bwd_f32"]
+    )
+
+
+def test_library_exports_every_declared_symbol(lib):
+    from unsamflow_amd import _lib
+
+    out = subprocess.run(["nm", "-D", "--defined-only", str(_lib.library_path())], capture_output=True,
+                         text=True, check=True).stdout
+    exported = set(re.findall(r"\bT (usf_\w+)", out))
+    for s in declared_symbols():
+        assert s in exported, s
+        assert hasattr(lib, s)
+    assert set(_lib.EXPORTED_SYMBOLS) == set(declared_symbols())
+
+
+def test_abi_version(lib):
+    from unsamflow_amd import _lib
+
+    assert lib.usf_abi_version() == _lib.ABI_VERSION == 1
+
+
+def test_no_torch_types_in_abi():
+    text = HEADER.read_text()
+    for bad in ("at::", "torch", "Tensor", "c10"):
+        # the header only mentions torch in prose comments
+        code = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+        assert bad not in code
+
+
+@pytest.mark.parametrize(
+    "call,needle",
+    [
+        (lambda L: L.usf_corr_fwd_f32(1, 1, 1, 0, 4, 4, 4, 4, None), "non-positive shape"),
+        (lambda L: L.usf_corr_fwd_f32(1, 1, 1, 1, 4, 4, 4, 5, None), "max_displacement 5"),
+        (lambda L: L.usf_corr_fwd_f32(None, 1, 1, 1, 4, 4, 4, 4, None), "null pointer"),
+        (lambda L: L.usf_corr_bwd_f32(1, 1, None, 1, 1, 1, 4, 4, 4, 4, None), "null input"),
+        (lambda L: L.usf_corr_bwd_f32(1, 1, 1, 1, 1, 1, 4, 4, 4, 0, None), "max_displacement 0"),
+        (lambda L: L.usf_warp_fwd_f32(1, 1, 32, 1, 1, 3, 4, 4, 7, None), "pad_mode 7"),
+        (lambda L: L.usf_warp_fwd_f32(1, 1, 3, 1, 2, 3, 4, 4, 1, None), "batch stride"),
+        (lambda L: L.usf_warp_bwd_f32(1, None, 32, 1, 1, 1, 1, 3, 4, 4, 1, None), "null input"),
+        (lambda L: L.usf_warp_bwd_f32(1, 1, 32, 1, 1, 1, 1, 3, -4, 4, 1, None), "non-positive"),
+        (lambda L: L.usf_corr_fwd_f32(1, 1, 1, 1, 70000, 200, 200, 4, None), "too large"),
+    ],
+)
+def test_invalid_arguments_rejected_without_launch(lib, call, needle):
+    rc = call(lib)
+    assert rc == -1
+    msg = lib.usf_last_error_string().decode()
+    assert needle in msg, msg
+
+
+def test_error_string_cleared_on_next_call(lib):
+    assert lib.usf_corr_fwd_f32(1, 1, 1, 0, 4, 4, 4, 4, None) == -1
+    assert lib.usf_last_error_string() != b""
+    # a warp bwd with neither output requested is a valid no-op (no launch)
+    assert lib.usf_warp_bwd_f32(1, 1, 32, 1, None, None, 1, 3, 4, 4, 1, None) == 0
+    assert lib.usf_last_error_string() == b""
+
+
+def test_ctypes_signatures_match_header():
+    """argtype counts of the ctypes binding equal the C prototypes' parameter counts."""
+    from unsamflow_amd import _lib
+
+    text = re.sub(r"/\*.*?\*/", "", HEADER.read_text(), flags=re.S)
+    for name, (argtypes, _) in _lib._SIGNATURES.items():
+        m = re.search(name + r"\s*\(([^)]*)\)", text)
+        params = [p for p in m.group(1).split(",") if p.strip() and p.strip() != "void"]
+        assert len(params) == len(argtypes), name
+    assert ctypes.sizeof(ctypes.c_longlong) == 8

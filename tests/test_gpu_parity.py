@@ -1,0 +1,281 @@
+"""Parity of the HIP kernels (through the C ABI) with the oracle and the
+reference's golden vectors. Runs on an MI355X: ``pytest -m gpu``.
+
+Tolerances (fp32; stated per SURVEY.md §8c):
+* correlation fwd/bwd: atol=1e-5, rtol=1e-5 vs the reference / fp64 oracle;
+* warp fwd: atol=1e-5; warp grad_flow: atol=1e-4, rtol=1e-5; warp grad_x:
+  atol=1e-5 (fp32 atomics: summation order is not fixed).
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden_files, load_golden
+from oracle import hashrng
+from oracle.corr import corr_backward_np, corr_forward_np
+from oracle.warp import warp_backward_np, warp_forward_np
+
+pytestmark = pytest.mark.gpu
+
+CORR_ATOL = 1e-5
+CORR_RTOL = 1e-5
+
+
+def _dev(a, dev):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+
+
+def _np(t):
+    return t.detach().cpu().numpy()
+
+
+# ------------------------------------------------------------ correlation --
+@pytest.mark.parametrize("name", golden_files("corr_"))
+def test_corr_fwd_bwd_vs_reference_golden(hip_device, name):
+    from unsamflow_amd import ops
+
+    z = load_golden(name)
+    d = int(z["d"])
+    x1, x2, g = _dev(z["x1"], hip_device), _dev(z["x2"], hip_device), _dev(z["gout"], hip_device)
+    out = ops.corr_forward(x1, x2, d)
+    gx1, gx2 = ops.corr_backward(x1, x2, g, d)
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(_np(out), z["out"], atol=CORR_ATOL, rtol=CORR_RTOL)
+    np.testing.assert_allclose(_np(gx1), z["gx1"], atol=CORR_ATOL, rtol=CORR_RTOL)
+    np.testing.assert_allclose(_np(gx2), z["gx2"], atol=CORR_ATOL, rtol=CORR_RTOL)
+
+
+# shapes of every PWCLite call site (KITTI + Sintel levels, mask-feature C=32),
+# plus ragged edges; B kept small so the fp64 oracle stays fast
+FUZZ_SHAPES = [
+    (2, 192, 4, 13), (2, 128, 8, 26), (1, 96, 16, 52), (1, 64, 32, 104), (1, 32, 64, 208),
+    (1, 192, 7, 16), (1, 128, 14, 32), (1, 32, 28, 64), (1, 32, 4, 13),
+    (3, 5, 17, 33), (1, 1, 1, 1), (1, 17, 2, 70), (2, 40, 9, 9), (1, 8, 65, 3),
+]
+
+
+@pytest.mark.parametrize("shape", FUZZ_SHAPES)
+def test_corr_vs_oracle_call_site_shapes(hip_device, shape):
+    from unsamflow_amd import ops
+
+    B, C, H, W = shape
+    seed = B * 1000003 + C * 1009 + H * 31 + W
+    x1 = hashrng.normal(shape, seed)
+    x2 = hashrng.normal(shape, seed + 1)
+    g = hashrng.normal((B, 81, H, W), seed + 2)
+    t1, t2, tg = _dev(x1, hip_device), _dev(x2, hip_device), _dev(g, hip_device)
+    out = ops.corr_forward(t1, t2, 4)
+    gx1, gx2 = ops.corr_backward(t1, t2, tg, 4)
+    np.testing.assert_allclose(_np(out), corr_forward_np(x1, x2, 4), atol=CORR_ATOL, rtol=CORR_RTOL)
+    r1, r2 = corr_backward_np(x1, x2, g, 4)
+    np.testing.assert_allclose(_np(gx1), r1, atol=CORR_ATOL, rtol=CORR_RTOL)
+    np.testing.assert_allclose(_np(gx2), r2, atol=CORR_ATOL, rtol=CORR_RTOL)
+
+
+@pytest.mark.parametrize("d", [1, 2, 3])
+def test_corr_other_displacements_vs_oracle(hip_device, d):
+    from unsamflow_amd import ops
+
+    shape = (2, 24, 19, 45)
+    x1 = hashrng.normal(shape, 11 + d)
+    x2 = hashrng.normal(shape, 22 + d)
+    K = 2 * d + 1
+    g = hashrng.normal((2, K * K, 19, 45), 33 + d)
+    t1, t2 = _dev(x1, hip_device), _dev(x2, hip_device)
+    out = ops.corr_forward(t1, t2, d)
+    gx1, gx2 = ops.corr_backward(t1, t2, _dev(g, hip_device), d)
+    np.testing.assert_allclose(_np(out), corr_forward_np(x1, x2, d), atol=CORR_ATOL, rtol=CORR_RTOL)
+    r1, r2 = corr_backward_np(x1, x2, g, d)
+    np.testing.assert_allclose(_np(gx1), r1, atol=CORR_ATOL, rtol=CORR_RTOL)
+    np.testing.assert_allclose(_np(gx2), r2, atol=CORR_ATOL, rtol=CORR_RTOL)
+
+
+@pytest.mark.parametrize("name", golden_files("corrbig_"))
+def test_corr_full_size_configs_vs_reference(hip_device, name):
+    """BASELINE configs 1 and 2 at full size: reference sums + 4096 sampled elements."""
+    from unsamflow_amd import ops
+
+    z = load_golden(name)
+    B, C, H, W, d, seed = (int(v) for v in z["shape"])
+    x1 = _dev(hashrng.normal((B, C, H, W), seed), hip_device)
+    x2 = _dev(hashrng.normal((B, C, H, W), seed + 1), hip_device)
+    g = _dev(hashrng.normal((B, (2 * d + 1) ** 2, H, W), seed + 2), hip_device)
+    out = ops.corr_forward(x1, x2, d)
+    gx1, gx2 = ops.corr_backward(x1, x2, g, d)
+    for key, t in (("out", out), ("gx1", gx1), ("gx2", gx2)):
+        flat = t.reshape(-1)
+        idx = torch.from_numpy(z[key + "_idx"]).to(hip_device)
+        np.testing.assert_allclose(_np(flat[idx]), z[key + "_val"], atol=CORR_ATOL, rtol=CORR_RTOL)
+        s = flat.double().sum().item()
+        a = flat.double().abs().sum().item()
+        assert abs(s - float(z[key + "_sum"])) <= 1e-5 * float(z[key + "_abssum"]), key
+        assert abs(a - float(z[key + "_abssum"])) <= 1e-5 * float(z[key + "_abssum"]), key
+
+
+def test_corr_backward_is_deterministic(hip_device):
+    from unsamflow_amd import ops
+
+    shape = (2, 64, 32, 104)
+    x1 = _dev(hashrng.normal(shape, 5), hip_device)
+    x2 = _dev(hashrng.normal(shape, 6), hip_device)
+    g = _dev(hashrng.normal((2, 81, 32, 104), 7), hip_device)
+    a1, a2 = ops.corr_backward(x1, x2, g, 4)
+    b1, b2 = ops.corr_backward(x1, x2, g, 4)
+    assert torch.equal(a1, b1) and torch.equal(a2, b2)
+
+
+def test_corr_properties_at_kitti_l4_full_batch(hip_device):
+    """Size-independent properties at the largest call site (B=8, C=32, 64x208):
+    bilinearity of the forward, the adjoint identity <corr(x1,x2), g> =
+    <x1, gx1> = <x2, gx2>, and the zero-displacement channel == channel mean."""
+    from unsamflow_amd import ops
+
+    shape = (8, 32, 64, 208)
+    x1 = _dev(hashrng.normal(shape, 91), hip_device)
+    x2 = _dev(hashrng.normal(shape, 92), hip_device)
+    x3 = _dev(hashrng.normal(shape, 93), hip_device)
+    g = _dev(hashrng.normal((8, 81, 64, 208), 94), hip_device)
+    o12 = ops.corr_forward(x1, x2, 4)
+    o13 = ops.corr_forward(x1, x3, 4)
+    o1s = ops.corr_forward(x1, 2.0 * x2 - 0.5 * x3, 4)
+    torch.testing.assert_close(o1s, 2.0 * o12 - 0.5 * o13, atol=1e-5, rtol=1e-5)
+    torch.testing.assert_close(o12[:, 40], (x1 * x2).mean(1), atol=1e-6, rtol=1e-5)
+    gx1, gx2 = ops.corr_backward(x1, x2, g, 4)
+    lhs = (o12.double() * g.double()).sum()
+    r1 = (x1.double() * gx1.double()).sum()
+    r2 = (x2.double() * gx2.double()).sum()
+    scale = (o12.double().abs() * g.double().abs()).sum()
+    assert abs(lhs - r1) <= 1e-6 * scale
+    assert abs(lhs - r2) <= 1e-6 * scale
+
+
+def test_correlation_module_autograd_and_inplace_relu(hip_device):
+    """Module path as PWCLite uses it: in-place LeakyReLU on the output, then backward."""
+    from unsamflow_amd.correlation import Correlation
+
+    shape = (2, 16, 12, 20)
+    x1 = hashrng.normal(shape, 71)
+    x2 = hashrng.normal(shape, 72)
+    g = hashrng.normal((2, 81, 12, 20), 73)
+    t1 = _dev(x1, hip_device).requires_grad_(True)
+    t2 = _dev(x2, hip_device).requires_grad_(True)
+    corr = Correlation(pad_size=4, kernel_size=1, max_displacement=4, stride1=1, stride2=1, corr_multiply=1)
+    out = torch.nn.LeakyReLU(0.1, inplace=True)(corr(t1, t2))
+    out.backward(_dev(g, hip_device))
+    ref = corr_forward_np(x1, x2, 4)
+    np.testing.assert_allclose(_np(out), np.where(ref > 0, ref, 0.1 * ref), atol=CORR_ATOL, rtol=CORR_RTOL)
+    gr = np.where(ref > 0, g, 0.1 * g)
+    r1, r2 = corr_backward_np(x1, x2, gr, 4)
+    np.testing.assert_allclose(_np(t1.grad), r1, atol=CORR_ATOL, rtol=CORR_RTOL)
+    np.testing.assert_allclose(_np(t2.grad), r2, atol=CORR_ATOL, rtol=CORR_RTOL)
+
+
+def test_correlation_only_one_input_requires_grad(hip_device):
+    from unsamflow_amd.correlation_native import Correlation
+
+    t1 = _dev(hashrng.normal((1, 8, 6, 9), 1), hip_device).requires_grad_(True)
+    t2 = _dev(hashrng.normal((1, 8, 6, 9), 2), hip_device)
+    Correlation(4)(t1, t2).sum().backward()
+    assert t1.grad is not None and t2.grad is None
+
+
+def test_corr_noncontiguous_inputs(hip_device):
+    from unsamflow_amd import ops
+
+    base = _dev(hashrng.normal((2, 20, 10, 12), 3), hip_device)
+    x1 = base[:, ::2]
+    x2 = base[:, 1::2]
+    out = ops.corr_forward(x1, x2, 4)
+    ref = corr_forward_np(_np(x1), _np(x2), 4)
+    np.testing.assert_allclose(_np(out), ref, atol=CORR_ATOL, rtol=CORR_RTOL)
+
+
+# ------------------------------------------------------------------- warp --
+def _warp_case(z, dev):
+    flow_full = _dev(z["flow_full"], dev)
+    flow = flow_full[:, 2:] if int(z["slice"]) else flow_full
+    return _dev(z["x"], dev), flow_full, flow, str(z["pad"])
+
+
+@pytest.mark.parametrize("name", golden_files("warp_"))
+def test_warp_fwd_bwd_vs_reference_golden(hip_device, name):
+    from unsamflow_amd.warp_utils import flow_warp
+
+    z = load_golden(name)
+    x, flow_full, flow, pad = _warp_case(z, hip_device)
+    x.requires_grad_(True)
+    flow_full.requires_grad_(True)
+    fl = flow_full[:, 2:] if int(z["slice"]) else flow_full
+    out = flow_warp(x, fl, pad=pad)
+    out.backward(_dev(z["gout"], hip_device))
+    gflow = _np(flow_full.grad)
+    if int(z["slice"]):
+        assert np.all(gflow[:, :2] == 0)
+        gflow = gflow[:, 2:]
+    np.testing.assert_allclose(_np(out), z["out"], atol=1e-5, rtol=0)
+    np.testing.assert_allclose(_np(x.grad), z["gx"], atol=1e-5, rtol=1e-5)
+    np.testing.assert_allclose(gflow, z["gflow"], atol=1e-4, rtol=1e-5)
+
+
+@pytest.mark.parametrize("pad", ["border", "zeros"])
+@pytest.mark.parametrize("shape,scale", [((8, 32, 64, 208), 3.0), ((2, 3, 256, 832), 40.0), ((4, 128, 8, 26), 1.5)])
+def test_warp_vs_oracle_call_site_shapes(hip_device, pad, shape, scale):
+    from unsamflow_amd import ops
+
+    B, C, H, W = shape
+    seed = C * 7 + H
+    x = hashrng.uniform(shape, seed)
+    flow = hashrng.symmetric((B, 2, H, W), seed + 1, scale)
+    g = hashrng.normal(shape, seed + 2)
+    tx, tf, tg = _dev(x, hip_device), _dev(flow, hip_device), _dev(g, hip_device)
+    out = ops.warp_forward(tx, tf, pad)
+    gx, gf = ops.warp_backward(tx, tf, tg, pad)
+    np.testing.assert_allclose(_np(out), warp_forward_np(x, flow, pad), atol=1e-5, rtol=0)
+    rx, rf = warp_backward_np(x, flow, g, pad)
+    np.testing.assert_allclose(_np(gx), rx, atol=1e-5, rtol=1e-5)
+    np.testing.assert_allclose(_np(gf), rf, atol=1e-4, rtol=1e-5)
+
+
+def test_warp_loss_style_slices_and_flow_only_grad(hip_device):
+    """flow_loss.py:130-131: image warps by channel slices of a [B,4,h,w] flow,
+    gradient only w.r.t. the flow (images do not require grad)."""
+    from unsamflow_amd.warp_utils import flow_warp
+
+    B, H, W = 2, 64, 208
+    im = _dev(hashrng.uniform((B, 3, H, W), 1), hip_device)
+    flow4 = _dev(hashrng.symmetric((B, 4, H, W), 2, 5.0), hip_device).requires_grad_(True)
+    g1 = hashrng.normal((B, 3, H, W), 3)
+    g2 = hashrng.normal((B, 3, H, W), 4)
+    o1 = flow_warp(im, flow4[:, :2], pad="border")
+    o2 = flow_warp(im, flow4[:, 2:], pad="border")
+    (o1 * _dev(g1, hip_device) + o2 * _dev(g2, hip_device)).sum().backward()
+    f = _np(flow4.detach())
+    imn = _np(im)
+    _, r1 = warp_backward_np(imn, f[:, :2], g1, "border", need_x=False)
+    _, r2 = warp_backward_np(imn, f[:, 2:], g2, "border", need_x=False)
+    np.testing.assert_allclose(_np(flow4.grad), np.concatenate([r1, r2], 1), atol=1e-4, rtol=1e-5)
+    np.testing.assert_allclose(_np(o1), warp_forward_np(imn, f[:, :2]), atol=1e-5, rtol=0)
+
+
+def test_warp_zero_flow_is_identity(hip_device):
+    from unsamflow_amd import ops
+
+    x = _dev(hashrng.uniform((3, 16, 33, 47), 9), hip_device)
+    z = torch.zeros(3, 2, 33, 47, device=hip_device)
+    for pad in ("border", "zeros"):
+        torch.testing.assert_close(ops.warp_forward(x, z, pad), x, atol=1e-6, rtol=0)
+
+
+def test_warp_integer_shift_matches_roll(hip_device):
+    """An integer flow is an exact shift (bilinear weights 0/1) with border clamp."""
+    from unsamflow_amd import ops
+
+    x = _dev(hashrng.uniform((1, 4, 20, 30), 10), hip_device)
+    flow = torch.zeros(1, 2, 20, 30, device=hip_device)
+    flow[:, 0] = 3.0
+    flow[:, 1] = -2.0
+    out = ops.warp_forward(x, flow, "border")
+    cols = torch.clamp(torch.arange(30, device=hip_device) + 3, 0, 29)
+    rows = torch.clamp(torch.arange(20, device=hip_device) - 2, 0, 19)
+    ref = x[:, :, rows][:, :, :, cols]
+    torch.testing.assert_close(out, ref, atol=1e-6, rtol=0)

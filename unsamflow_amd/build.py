@@ -1,0 +1,95 @@
+"""Build libunsamflow_hip.so in-tree with hipcc for gfx950.
+
+The library is a plain C-ABI shared object (include/unsamflow_hip.h); it is
+loaded with ctypes by :mod:`unsamflow_amd._lib`. No torch headers are used, so
+the build needs only hipcc (cross-compiles without a GPU).
+
+Usage: ``python -m unsamflow_amd.build [--force] [--verbose]``
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+PKG_DIR = Path(__file__).resolve().parent
+CSRC = PKG_DIR / "csrc"
+LIB_DIR = PKG_DIR / "lib"
+LIB_PATH = LIB_DIR / "libunsamflow_hip.so"
+INCLUDE_DIR = PKG_DIR.parent / "include"
+
+ARCH = os.environ.get("USF_OFFLOAD_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+
+SOURCES = ["corr.hip", "warp.hip", "capi.cpp"]
+HEADERS = ["usf_common.h"]
+
+COMMON_FLAGS = [
+    "-O3",
+    "-std=c++17",
+    "-fPIC",
+    f"--offload-arch={ARCH}",
+    "-Wall",
+    "-Wno-unused-function",
+    f"-I{INCLUDE_DIR}",
+]
+
+
+def _stale(target: Path, deps: list[Path]) -> bool:
+    if not target.exists():
+        return True
+    t = target.stat().st_mtime
+    return any(d.stat().st_mtime > t for d in deps)
+
+
+def build_library(force: bool = False, verbose: bool = False) -> Path:
+    """Compile every HIP source to an object file and link the shared library.
+
+    Returns the path of the built library. Raises ``RuntimeError`` with the
+    compiler output on failure.
+    """
+    LIB_DIR.mkdir(exist_ok=True)
+    obj_dir = LIB_DIR / "obj"
+    obj_dir.mkdir(exist_ok=True)
+    headers = [CSRC / h for h in HEADERS] + [INCLUDE_DIR / "unsamflow_hip.h"]
+    objs = []
+    for src in SOURCES:
+        s = CSRC / src
+        o = obj_dir / (s.stem + ".o")
+        objs.append(o)
+        if force or _stale(o, [s] + headers):
+            lang = ["-x", "hip"] if src.endswith(".hip") else []
+            cmd = [HIPCC, *COMMON_FLAGS, *lang, "-c", str(s), "-o", str(o)]
+            _run(cmd, verbose)
+    if force or _stale(LIB_PATH, objs):
+        tmp = LIB_PATH.with_suffix(".so.tmp")
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, objs), "-o", str(tmp)]
+        _run(cmd, verbose)
+        os.replace(tmp, LIB_PATH)
+    return LIB_PATH
+
+
+def _run(cmd: list[str], verbose: bool) -> None:
+    if verbose:
+        print("+", " ".join(cmd), flush=True)
+    p = subprocess.run(cmd, capture_output=True, text=True)
+    if p.returncode != 0:
+        raise RuntimeError(f"hipcc failed ({p.returncode}):\n{' '.join(cmd)}\n{p.stdout}\n{p.stderr}")
+    if verbose and (p.stdout or p.stderr):
+        print(p.stdout + p.stderr, flush=True)
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("--verbose", "-v", action="store_true")
+    a = ap.parse_args(argv)
+    path = build_library(force=a.force, verbose=a.verbose)
+    print(path)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,130 @@
+// C ABI of libunsamflow_hip.so (declared in include/unsamflow_hip.h).
+// Argument validation + error reporting; the launches live in corr.hip / warp.hip.
+#include <hip/hip_runtime.h>
+
+#include <climits>
+#include <cstdarg>
+#include <cstdio>
+
+#include "../../include/unsamflow_hip.h"
+#include "usf_common.h"
+
+namespace usf {
+
+static thread_local char g_err[512] = "";
+
+void set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+
+void clear_error() { g_err[0] = '\0'; }
+
+static bool check_dims(const char* fn, int B, int C, int H, int W) {
+  if (B <= 0 || C <= 0 || H <= 0 || W <= 0) {
+    set_error("%s: non-positive shape B=%d C=%d H=%d W=%d", fn, B, C, H, W);
+    return false;
+  }
+  // per-sample element offsets are 32-bit inside the kernels
+  const long long per_sample = (long long)C * H * W;
+  if (per_sample > INT_MAX || (long long)H * W * 81 > INT_MAX) {
+    set_error("%s: per-sample tensor too large (C*H*W=%lld)", fn, per_sample);
+    return false;
+  }
+  return true;
+}
+
+static int finish(const char* fn, hipError_t e) {
+  if (e != hipSuccess) {
+    set_error("%s: HIP launch failed: %s (%d)", fn, hipGetErrorString(e), (int)e);
+    return (int)e;
+  }
+  return 0;
+}
+
+}  // namespace usf
+
+using namespace usf;
+
+extern "C" {
+
+int usf_abi_version(void) { return USF_ABI_VERSION; }
+
+const char* usf_last_error_string(void) { return g_err; }
+
+int usf_corr_fwd_f32(const float* x1, const float* x2, float* out, int B, int C, int H, int W,
+                     int d, void* stream) {
+  clear_error();
+  if (!check_dims("usf_corr_fwd_f32", B, C, H, W)) return USF_EINVAL;
+  if (d < 1 || d > 4) {
+    set_error("usf_corr_fwd_f32: max_displacement %d not in [1,4]", d);
+    return USF_EINVAL;
+  }
+  if (!x1 || !x2 || !out) {
+    set_error("usf_corr_fwd_f32: null pointer");
+    return USF_EINVAL;
+  }
+  return finish("usf_corr_fwd_f32",
+                corr_fwd_launch(x1, x2, out, B, C, H, W, d, (hipStream_t)stream));
+}
+
+int usf_corr_bwd_f32(const float* x1, const float* x2, const float* gout, float* gx1,
+                     float* gx2, int B, int C, int H, int W, int d, void* stream) {
+  clear_error();
+  if (!check_dims("usf_corr_bwd_f32", B, C, H, W)) return USF_EINVAL;
+  if (d < 1 || d > 4) {
+    set_error("usf_corr_bwd_f32: max_displacement %d not in [1,4]", d);
+    return USF_EINVAL;
+  }
+  if (!gout || (gx1 && !x2) || (gx2 && !x1)) {
+    set_error("usf_corr_bwd_f32: null input pointer");
+    return USF_EINVAL;
+  }
+  return finish("usf_corr_bwd_f32",
+                corr_bwd_launch(x1, x2, gout, gx1, gx2, B, C, H, W, d, (hipStream_t)stream));
+}
+
+int usf_warp_fwd_f32(const float* x, const float* flow, long long flow_bstride, float* out,
+                     int B, int C, int H, int W, int pad_mode, void* stream) {
+  clear_error();
+  if (!check_dims("usf_warp_fwd_f32", B, C, H, W)) return USF_EINVAL;
+  if (pad_mode != USF_PAD_ZEROS && pad_mode != USF_PAD_BORDER) {
+    set_error("usf_warp_fwd_f32: unknown pad_mode %d", pad_mode);
+    return USF_EINVAL;
+  }
+  if (!x || !flow || !out) {
+    set_error("usf_warp_fwd_f32: null pointer");
+    return USF_EINVAL;
+  }
+  if (flow_bstride < 2LL * H * W && B > 1) {
+    set_error("usf_warp_fwd_f32: flow batch stride %lld < 2*H*W", flow_bstride);
+    return USF_EINVAL;
+  }
+  return finish("usf_warp_fwd_f32", warp_fwd_launch(x, flow, flow_bstride, out, B, C, H, W,
+                                                    pad_mode, (hipStream_t)stream));
+}
+
+int usf_warp_bwd_f32(const float* x, const float* flow, long long flow_bstride,
+                     const float* gout, float* gx, float* gflow, int B, int C, int H, int W,
+                     int pad_mode, void* stream) {
+  clear_error();
+  if (!check_dims("usf_warp_bwd_f32", B, C, H, W)) return USF_EINVAL;
+  if (pad_mode != USF_PAD_ZEROS && pad_mode != USF_PAD_BORDER) {
+    set_error("usf_warp_bwd_f32: unknown pad_mode %d", pad_mode);
+    return USF_EINVAL;
+  }
+  if (!flow || !gout || (gflow && !x)) {
+    set_error("usf_warp_bwd_f32: null input pointer");
+    return USF_EINVAL;
+  }
+  if (flow_bstride < 2LL * H * W && B > 1) {
+    set_error("usf_warp_bwd_f32: flow batch stride %lld < 2*H*W", flow_bstride);
+    return USF_EINVAL;
+  }
+  return finish("usf_warp_bwd_f32", warp_bwd_launch(x, flow, flow_bstride, gout, gx, gflow, B,
+                                                    C, H, W, pad_mode, (hipStream_t)stream));
+}
+
+}  // extern "C"

@@ -1,0 +1,371 @@
+// Local correlation (cost volume) forward / backward for gfx950 (CDNA4).
+//
+// Semantics (fp32, NCHW, displacement radius d, K = 2d+1, KK = K*K):
+//   out[b, dy*K+dx, y, x] = (1/C) sum_c x1[b,c,y,x] * X2(b,c, y+dy-d, x+dx-d)
+//   gx1[b,c,y,x] = (1/C) sum_k g[b,k,y,x] * X2(b,c, y+dy_k-d, x+dx_k-d)
+//   gx2[b,c,y,x] = (1/C) sum_k G(b,k, y-dy_k+d, x-dx_k+d) * X1(b,c, y-dy_k+d, x-dx_k+d)
+// with X*, G = 0 outside [0,H)x[0,W). This is correlation_native.py:13-23
+// (zero pad :16, 81 slice-products :18-21, channel mean :21, concat order :23)
+// and the CUDA plugin's correlation_forward / correlation_backward_input{1,2}
+// (correlation_cuda_kernel.cu:41-114, :116-207, :209-300) restricted to
+// kernel_size=1, stride1=stride2=1, pad=d, which is what pwclite.py:208-215 uses.
+//
+// Design (MI355X-first, not a translation of the CUDA kernels):
+//  * Forward: one workgroup = one output tile (TH rows x TW cols) x NDY
+//    displacement rows. Wave w owns displacement row dyb+w; lane l owns PX
+//    consecutive output pixels (row l/SEGX, segment l%SEGX). A channel stage of
+//    CC channels of the x1 tile and the (TH+NDY-1) x (TW+2d) x2 halo is staged
+//    in LDS (coalesced dword loads, zero fill = the zero padding), then each
+//    lane keeps K*PX accumulators in VGPRs and reads one x1 segment and one
+//    x2 window (PX+2d floats) per channel with ds_read_b128: K*PX FMAs per
+//    (2*PX+2d) LDS floats. No cross-lane reduction (the channel sum is a
+//    per-lane FMA chain), so no shared prod_sum/serial reduction as in the
+//    reference (.cu:84-109).
+//  * Backward: deterministic gather form, no atomics. gx1 and gx2 are the
+//    same kernel (G2 template flag): the output channel is independent, so a
+//    workgroup owns one tile x CC channels; wave w owns displacement rows
+//    w, w+NW, ...; per displacement row the lane loads its K*PX slice of g
+//    (coalesced along x) once and streams CC channels of the staged x halo
+//    from LDS. The NW per-wave partial sums are combined through LDS (which
+//    aliases the staging buffer) and written once, coalesced.
+#include "usf_common.h"
+
+namespace usf {
+namespace {
+
+// ---------------------------------------------------------------- forward --
+template <int D, int PX, int SEGX, int NDY, int CC>
+struct FwdCfg {
+  static constexpr int K = 2 * D + 1;
+  static constexpr int TW = SEGX * PX;          // tile width (pixels)
+  static constexpr int TH = 64 / SEGX;          // tile height (rows)
+  static constexpr int NT = 64 * NDY;           // threads per workgroup
+  static constexpr int NDYG = (K + NDY - 1) / NDY;
+  static constexpr int R2 = TH + NDY - 1;       // staged x2 rows
+  static constexpr int C2 = TW + 2 * D;         // staged x2 cols
+  static constexpr int WIN = round_up(PX + 2 * D, 4);
+  static constexpr int XS = round_up(C2, 4) + 4;  // LDS row stride (floats)
+  static constexpr int S1N = CC * TH * TW;
+  static constexpr int S2N = CC * R2 * XS + WIN;  // + tail pad for window over-read
+  static_assert(PX % 4 == 0, "PX must be a multiple of 4 (ds_read_b128)");
+  static_assert(64 % SEGX == 0, "SEGX must divide 64");
+};
+
+template <int D, int PX, int SEGX, int NDY, int CC>
+__global__ __launch_bounds__(64 * NDY) void corr_fwd_kernel(const float* __restrict__ x1,
+                                                            const float* __restrict__ x2,
+                                                            float* __restrict__ out, int C,
+                                                            int H, int W, int tiles_x) {
+  using F = FwdCfg<D, PX, SEGX, NDY, CC>;
+  constexpr int K = F::K, TW = F::TW, TH = F::TH, NT = F::NT, R2 = F::R2, C2 = F::C2;
+  constexpr int WIN = F::WIN, XS = F::XS;
+  __shared__ __attribute__((aligned(16))) float s1[F::S1N];
+  __shared__ __attribute__((aligned(16))) float s2[F::S2N];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int dyb = blockIdx.x * NDY;
+  const int tile = blockIdx.y;
+  const int b = blockIdx.z;
+  const int ty = tile / tiles_x;
+  const int tx = tile - ty * tiles_x;
+  const int y0 = ty * TH, x0 = tx * TW;
+  const int r = lane / SEGX, q = lane % SEGX;
+  const int dy = dyb + wave;
+  const bool active = dy < K;
+
+  const int HW = H * W;
+  const float* x1b = x1 + (size_t)b * C * HW;
+  const float* x2b = x2 + (size_t)b * C * HW;
+  const int gy2 = y0 + dyb - D;  // image row of staged x2 row 0
+  const int gx2 = x0 - D;        // image col of staged x2 col 0
+
+  float acc[K][PX];
+#pragma unroll
+  for (int j = 0; j < K; ++j)
+#pragma unroll
+    for (int i = 0; i < PX; ++i) acc[j][i] = 0.f;
+
+  for (int c0 = 0; c0 < C; c0 += CC) {
+    // stage x1 tile [CC][TH][TW]
+    for (int e = tid; e < F::S1N; e += NT) {
+      const int c = e / (TH * TW);
+      const int rem = e - c * (TH * TW);
+      const int rr = rem / TW;
+      const int cc = rem - rr * TW;
+      const int gc = c0 + c, gy = y0 + rr, gx = x0 + cc;
+      float v = 0.f;
+      if (gc < C && gy < H && gx < W) v = x1b[gc * HW + gy * W + gx];
+      s1[e] = v;
+    }
+    // stage x2 halo [CC][R2][C2] (zero outside the image == the zero padding)
+    for (int e = tid; e < CC * R2 * C2; e += NT) {
+      const int c = e / (R2 * C2);
+      const int rem = e - c * (R2 * C2);
+      const int rr = rem / C2;
+      const int cc = rem - rr * C2;
+      const int gc = c0 + c, gy = gy2 + rr, gx = gx2 + cc;
+      float v = 0.f;
+      if (gc < C && (unsigned)gy < (unsigned)H && (unsigned)gx < (unsigned)W)
+        v = x2b[gc * HW + gy * W + gx];
+      s2[c * (R2 * XS) + rr * XS + cc] = v;
+    }
+    __syncthreads();
+    if (active) {
+#pragma unroll 2
+      for (int c = 0; c < CC; ++c) {
+        float a[PX], w[WIN];
+        const float4* p1 =
+            reinterpret_cast<const float4*>(s1 + c * (TH * TW) + r * TW + q * PX);
+#pragma unroll
+        for (int i = 0; i < PX / 4; ++i) {
+          const float4 t = p1[i];
+          a[4 * i] = t.x; a[4 * i + 1] = t.y; a[4 * i + 2] = t.z; a[4 * i + 3] = t.w;
+        }
+        const float4* p2 =
+            reinterpret_cast<const float4*>(s2 + c * (R2 * XS) + (r + wave) * XS + q * PX);
+#pragma unroll
+        for (int i = 0; i < WIN / 4; ++i) {
+          const float4 t = p2[i];
+          w[4 * i] = t.x; w[4 * i + 1] = t.y; w[4 * i + 2] = t.z; w[4 * i + 3] = t.w;
+        }
+#pragma unroll
+        for (int dx = 0; dx < K; ++dx)
+#pragma unroll
+          for (int i = 0; i < PX; ++i) acc[dx][i] = fmaf(a[i], w[i + dx], acc[dx][i]);
+      }
+    }
+    __syncthreads();
+  }
+
+  if (!active) return;
+  const int y = y0 + r;
+  if (y >= H) return;
+  const int xb = x0 + q * PX;
+  const float cf = (float)C;
+  float* ob = out + ((size_t)b * K * K + (size_t)dy * K) * HW + y * W + xb;
+  const bool vec = ((W & 3) == 0) && (xb + PX <= W);
+#pragma unroll
+  for (int dx = 0; dx < K; ++dx) {
+    float* o = ob + dx * HW;
+    if (vec) {
+#pragma unroll
+      for (int i = 0; i < PX / 4; ++i)
+        reinterpret_cast<float4*>(o)[i] =
+            make_float4(acc[dx][4 * i] / cf, acc[dx][4 * i + 1] / cf, acc[dx][4 * i + 2] / cf,
+                        acc[dx][4 * i + 3] / cf);
+    } else {
+#pragma unroll
+      for (int i = 0; i < PX; ++i)
+        if (xb + i < W) o[i] = acc[dx][i] / cf;
+    }
+  }
+}
+
+template <int D, int PX, int SEGX, int NDY>
+hipError_t launch_fwd(const float* x1, const float* x2, float* out, int B, int C, int H, int W,
+                      hipStream_t s) {
+  using F = FwdCfg<D, PX, SEGX, NDY, 8>;
+  const int tiles_x = (W + F::TW - 1) / F::TW;
+  const int tiles_y = (H + F::TH - 1) / F::TH;
+  dim3 grid(F::NDYG, tiles_x * tiles_y, B);
+  hipLaunchKernelGGL((corr_fwd_kernel<D, PX, SEGX, NDY, 8>), grid, dim3(F::NT), 0, s, x1, x2,
+                     out, C, H, W, tiles_x);
+  return hipGetLastError();
+}
+
+template <int D>
+hipError_t fwd_dispatch(const float* x1, const float* x2, float* out, int B, int C, int H,
+                        int W, hipStream_t s) {
+  constexpr int K = 2 * D + 1;
+  // Prefer the big tile (8 px/lane, one workgroup covers every displacement
+  // row: x1/x2 staged once); fall back to smaller tiles / split displacement
+  // rows when that would leave most of the 256 CUs idle.
+  const long big = (long)B * ((W + 63) / 64) * ((H + 7) / 8);
+  if (big >= 256) return launch_fwd<D, 8, 8, K>(x1, x2, out, B, C, H, W, s);
+  const long mid = (long)B * ((W + 31) / 32) * ((H + 7) / 8);
+  if (mid >= 256) return launch_fwd<D, 4, 8, K>(x1, x2, out, B, C, H, W, s);
+  return launch_fwd<D, 4, 8, 3>(x1, x2, out, B, C, H, W, s);
+}
+
+// --------------------------------------------------------------- backward --
+template <int D, int PX, int SEGX, int NW, int CC>
+struct BwdCfg {
+  static constexpr int K = 2 * D + 1;
+  static constexpr int TW = SEGX * PX;
+  static constexpr int TH = 64 / SEGX;
+  static constexpr int NT = 64 * NW;
+  static constexpr int R = TH + 2 * D;           // staged rows
+  static constexpr int C2 = TW + 2 * D;          // staged cols
+  static constexpr int WIN = round_up(PX + 2 * D, 4);
+  static constexpr int XS = round_up(C2, 4) + 4;
+  static constexpr int SN = CC * R * XS + WIN;   // staging image
+  static constexpr int RN = NW * CC * TH * TW;   // per-wave partial sums (aliases staging)
+  static constexpr int SMN = SN > RN ? SN : RN;
+  static_assert(PX % 4 == 0, "PX must be a multiple of 4");
+};
+
+// G2 == false: gx1 from (g, x2).  G2 == true: gx2 from (g, x1).
+template <int D, int PX, int SEGX, int NW, int CC, bool G2>
+__global__ __launch_bounds__(64 * NW) void corr_bwd_kernel(const float* __restrict__ xs,
+                                                           const float* __restrict__ g,
+                                                           float* __restrict__ gx, int C, int H,
+                                                           int W, int tiles_x) {
+  using F = BwdCfg<D, PX, SEGX, NW, CC>;
+  constexpr int K = F::K, TW = F::TW, TH = F::TH, NT = F::NT, R = F::R, C2 = F::C2;
+  constexpr int WIN = F::WIN, XS = F::XS;
+  __shared__ __attribute__((aligned(16))) float sm[F::SMN];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int tile = blockIdx.x;
+  const int c0 = blockIdx.y * CC;
+  const int b = blockIdx.z;
+  const int ty = tile / tiles_x;
+  const int tx = tile - ty * tiles_x;
+  const int y0 = ty * TH, x0 = tx * TW;
+  const int r = lane / SEGX, q = lane % SEGX;
+  const int y = y0 + r;
+  const int xb = x0 + q * PX;
+
+  const int HW = H * W;
+  const float* xsb = xs + (size_t)b * C * HW;
+  const float* gb = g + (size_t)b * K * K * HW;
+
+  // stage xs rows [y0-D, y0+TH+D) x cols [x0-D, x0+TW+D) for CC channels
+  for (int e = tid; e < CC * R * C2; e += NT) {
+    const int c = e / (R * C2);
+    const int rem = e - c * (R * C2);
+    const int rr = rem / C2;
+    const int cc = rem - rr * C2;
+    const int gc = c0 + c, gy = y0 - D + rr, gxx = x0 - D + cc;
+    float v = 0.f;
+    if (gc < C && (unsigned)gy < (unsigned)H && (unsigned)gxx < (unsigned)W)
+      v = xsb[gc * HW + gy * W + gxx];
+    sm[c * (R * XS) + rr * XS + cc] = v;
+  }
+  __syncthreads();
+
+  float acc[CC][PX];
+#pragma unroll
+  for (int c = 0; c < CC; ++c)
+#pragma unroll
+    for (int i = 0; i < PX; ++i) acc[c][i] = 0.f;
+
+  for (int dy = wave; dy < K; dy += NW) {
+    float gv[K][PX];
+    if (!G2) {
+      // g at the output pixels themselves: g[b, dy*K+dx, y, xb+i]
+      const bool rowok = y < H;
+#pragma unroll
+      for (int dx = 0; dx < K; ++dx) {
+        const float* gp = gb + (dy * K + dx) * HW + y * W + xb;
+#pragma unroll
+        for (int i = 0; i < PX; ++i) gv[dx][i] = (rowok && xb + i < W) ? gp[i] : 0.f;
+      }
+    } else {
+      // g at the source pixels: g[b, dy*K+dx, y-(dy-D), xb+i-(dx-D)]
+      const int yy = y - dy + D;
+      const bool rowok = (unsigned)yy < (unsigned)H;
+#pragma unroll
+      for (int dx = 0; dx < K; ++dx) {
+        const int xx0 = xb - dx + D;
+        const float* gp = gb + (dy * K + dx) * HW + yy * W + xx0;
+#pragma unroll
+        for (int i = 0; i < PX; ++i)
+          gv[dx][i] = (rowok && (unsigned)(xx0 + i) < (unsigned)W) ? gp[i] : 0.f;
+      }
+    }
+    const int rs = G2 ? (2 * D - dy) : dy;
+    const float* srow = sm + (r + rs) * XS + q * PX;
+#pragma unroll
+    for (int c = 0; c < CC; ++c) {
+      float w[WIN];
+      const float4* p = reinterpret_cast<const float4*>(srow + c * (R * XS));
+#pragma unroll
+      for (int i = 0; i < WIN / 4; ++i) {
+        const float4 t = p[i];
+        w[4 * i] = t.x; w[4 * i + 1] = t.y; w[4 * i + 2] = t.z; w[4 * i + 3] = t.w;
+      }
+#pragma unroll
+      for (int dx = 0; dx < K; ++dx) {
+        const int cs = G2 ? (2 * D - dx) : dx;
+#pragma unroll
+        for (int i = 0; i < PX; ++i) acc[c][i] = fmaf(gv[dx][i], w[i + cs], acc[c][i]);
+      }
+    }
+  }
+  __syncthreads();  // every wave is done reading the staging image
+
+  float* rp = sm + wave * (CC * TH * TW) + r * TW + q * PX;
+#pragma unroll
+  for (int c = 0; c < CC; ++c)
+#pragma unroll
+    for (int i = 0; i < PX / 4; ++i)
+      reinterpret_cast<float4*>(rp + c * (TH * TW))[i] =
+          make_float4(acc[c][4 * i], acc[c][4 * i + 1], acc[c][4 * i + 2], acc[c][4 * i + 3]);
+  __syncthreads();
+
+  const float cf = (float)C;
+  float* gxb = gx + (size_t)b * C * HW;
+  for (int o = tid; o < CC * TH * TW; o += NT) {
+    float sum = 0.f;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) sum += sm[w * (CC * TH * TW) + o];
+    const int c = o / (TH * TW);
+    const int pix = o - c * (TH * TW);
+    const int yy = y0 + pix / TW;
+    const int xx = x0 + pix % TW;
+    if (c0 + c < C && yy < H && xx < W) gxb[(c0 + c) * HW + yy * W + xx] = sum / cf;
+  }
+}
+
+template <int D, bool G2>
+hipError_t launch_bwd(const float* xs, const float* g, float* gx, int B, int C, int H, int W,
+                      hipStream_t s) {
+  constexpr int PX = 4, SEGX = 8, NW = 3, CC = 16;
+  using F = BwdCfg<D, PX, SEGX, NW, CC>;
+  const int tiles_x = (W + F::TW - 1) / F::TW;
+  const int tiles_y = (H + F::TH - 1) / F::TH;
+  dim3 grid(tiles_x * tiles_y, (C + CC - 1) / CC, B);
+  hipLaunchKernelGGL((corr_bwd_kernel<D, PX, SEGX, NW, CC, G2>), grid, dim3(F::NT), 0, s, xs, g,
+                     gx, C, H, W, tiles_x);
+  return hipGetLastError();
+}
+
+template <int D>
+hipError_t bwd_dispatch(const float* x1, const float* x2, const float* g, float* gx1, float* gx2,
+                        int B, int C, int H, int W, hipStream_t s) {
+  hipError_t e = hipSuccess;
+  if (gx1) e = launch_bwd<D, false>(x2, g, gx1, B, C, H, W, s);
+  if (e == hipSuccess && gx2) e = launch_bwd<D, true>(x1, g, gx2, B, C, H, W, s);
+  return e;
+}
+
+}  // namespace
+
+hipError_t corr_fwd_launch(const float* x1, const float* x2, float* out, int B, int C, int H,
+                           int W, int d, hipStream_t s) {
+  switch (d) {
+    case 1: return fwd_dispatch<1>(x1, x2, out, B, C, H, W, s);
+    case 2: return fwd_dispatch<2>(x1, x2, out, B, C, H, W, s);
+    case 3: return fwd_dispatch<3>(x1, x2, out, B, C, H, W, s);
+    case 4: return fwd_dispatch<4>(x1, x2, out, B, C, H, W, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+hipError_t corr_bwd_launch(const float* x1, const float* x2, const float* gout, float* gx1,
+                           float* gx2, int B, int C, int H, int W, int d, hipStream_t s) {
+  switch (d) {
+    case 1: return bwd_dispatch<1>(x1, x2, gout, gx1, gx2, B, C, H, W, s);
+    case 2: return bwd_dispatch<2>(x1, x2, gout, gx1, gx2, B, C, H, W, s);
+    case 3: return bwd_dispatch<3>(x1, x2, gout, gx1, gx2, B, C, H, W, s);
+    case 4: return bwd_dispatch<4>(x1, x2, gout, gx1, gx2, B, C, H, W, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+}  // namespace usf

@@ -1,0 +1,31 @@
+// Shared helpers for the gfx950 kernels of libunsamflow_hip.so.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstddef>
+#include <cstdint>
+
+namespace usf {
+
+// Thread-local error slot behind usf_last_error_string().
+void set_error(const char* fmt, ...);
+void clear_error();
+
+// Round n up to a multiple of m (compile-time helper).
+__host__ __device__ constexpr int round_up(int n, int m) { return ((n + m - 1) / m) * m; }
+
+// Launchers implemented in corr.hip / warp.hip. They assume validated
+// arguments (capi.cpp checks shapes, d and pointers) and return the
+// hipError_t of the launch.
+hipError_t corr_fwd_launch(const float* x1, const float* x2, float* out, int B, int C,
+                           int H, int W, int d, hipStream_t s);
+hipError_t corr_bwd_launch(const float* x1, const float* x2, const float* gout,
+                           float* gx1, float* gx2, int B, int C, int H, int W, int d,
+                           hipStream_t s);
+hipError_t warp_fwd_launch(const float* x, const float* flow, long long flow_bstride,
+                           float* out, int B, int C, int H, int W, int pad_mode,
+                           hipStream_t s);
+hipError_t warp_bwd_launch(const float* x, const float* flow, long long flow_bstride,
+                           const float* gout, float* gx, float* gflow, int B, int C, int H,
+                           int W, int pad_mode, hipStream_t s);
+
+}  // namespace usf

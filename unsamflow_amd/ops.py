@@ -1,0 +1,161 @@
+"""Tensor-level entry points to the HIP kernels (no autograd).
+
+Each function validates its tensors, allocates the outputs with torch (the
+caching allocator owns all memory; the library never allocates), and launches
+on torch's current stream of the tensors' device. There is deliberately no
+CPU path: CPU tensors raise ``RuntimeError``.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+
+PAD_MODES = {"zeros": _lib.PAD_ZEROS, "border": _lib.PAD_BORDER}
+
+
+def _ptr(t: torch.Tensor | None) -> int | None:
+    return None if t is None else t.data_ptr()
+
+
+def _require_device_f32(name: str, t: torch.Tensor) -> None:
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name} must be a torch.Tensor, got {type(t).__name__}")
+    if t.device.type != "cuda":
+        raise RuntimeError(
+            f"unsamflow_amd: {name} is on {t.device}; the HIP kernels need tensors on a ROCm "
+            "device (there is no CPU path)"
+        )
+    if t.dtype != torch.float32:
+        raise TypeError(f"unsamflow_amd: {name} must be float32, got {t.dtype}")
+
+
+def _nchw(name: str, t: torch.Tensor) -> tuple[int, int, int, int]:
+    if t.dim() != 4:
+        raise ValueError(f"{name} must be 4-D NCHW, got shape {tuple(t.shape)}")
+    return tuple(t.shape)  # type: ignore[return-value]
+
+
+def corr_forward(x1: torch.Tensor, x2: torch.Tensor, max_displacement: int) -> torch.Tensor:
+    """Cost volume [B,(2d+1)^2,H,W] of x1 against x2 (correlation_native.py:13-23)."""
+    _require_device_f32("input1", x1)
+    _require_device_f32("input2", x2)
+    B, C, H, W = _nchw("input1", x1)
+    if x2.shape != x1.shape:
+        raise ValueError(f"input2 shape {tuple(x2.shape)} != input1 shape {tuple(x1.shape)}")
+    if x2.device != x1.device:
+        raise ValueError("input1 and input2 are on different devices")
+    d = int(max_displacement)
+    K = 2 * d + 1
+    x1c, x2c = x1.contiguous(), x2.contiguous()
+    out = torch.empty((B, K * K, H, W), device=x1.device, dtype=torch.float32)
+    lib = _lib.load()
+    with torch.cuda.device(x1.device):
+        rc = lib.usf_corr_fwd_f32(
+            x1c.data_ptr(), x2c.data_ptr(), out.data_ptr(), B, C, H, W, d, _lib.stream_handle(x1.device)
+        )
+    _lib.check(rc, "usf_corr_fwd_f32")
+    return out
+
+
+def corr_backward(
+    x1: torch.Tensor,
+    x2: torch.Tensor,
+    grad_out: torch.Tensor,
+    max_displacement: int,
+    need_x1: bool = True,
+    need_x2: bool = True,
+) -> tuple[torch.Tensor | None, torch.Tensor | None]:
+    """(grad_input1, grad_input2) of :func:`corr_forward`; deterministic."""
+    _require_device_f32("input1", x1)
+    _require_device_f32("input2", x2)
+    _require_device_f32("grad_output", grad_out)
+    B, C, H, W = _nchw("input1", x1)
+    d = int(max_displacement)
+    K = 2 * d + 1
+    if tuple(grad_out.shape) != (B, K * K, H, W):
+        raise ValueError(f"grad_output shape {tuple(grad_out.shape)} != {(B, K * K, H, W)}")
+    if not (need_x1 or need_x2):
+        return None, None
+    x1c, x2c, gc = x1.contiguous(), x2.contiguous(), grad_out.contiguous()
+    g1 = torch.empty_like(x1c) if need_x1 else None
+    g2 = torch.empty_like(x2c) if need_x2 else None
+    lib = _lib.load()
+    with torch.cuda.device(x1.device):
+        rc = lib.usf_corr_bwd_f32(
+            x1c.data_ptr(), x2c.data_ptr(), gc.data_ptr(), _ptr(g1), _ptr(g2),
+            B, C, H, W, d, _lib.stream_handle(x1.device),
+        )
+    _lib.check(rc, "usf_corr_bwd_f32")
+    return g1, g2
+
+
+def _flow_view(flow: torch.Tensor, B: int, H: int, W: int) -> tuple[torch.Tensor, int]:
+    """Flow tensor whose per-sample [2,H,W] block is dense, plus its batch stride.
+
+    A channel slice such as ``flow[:, :2]`` of a contiguous [B,4,H,W] tensor
+    (flow_loss.py:130-131) qualifies as-is (batch stride 4*H*W): no copy.
+    """
+    if tuple(flow.shape) != (B, 2, H, W):
+        raise ValueError(f"flow shape {tuple(flow.shape)} != {(B, 2, H, W)}")
+    s = flow.stride()
+    if s[1] == H * W and s[2] == W and s[3] == 1 and (B == 1 or s[0] >= 2 * H * W):
+        return flow, s[0] if B > 1 else 2 * H * W
+    flow = flow.contiguous()
+    return flow, 2 * H * W
+
+
+def warp_forward(x: torch.Tensor, flow: torch.Tensor, pad: str = "border") -> torch.Tensor:
+    """Bilinear backward warp of x by flow (warp_utils.py:97-106)."""
+    _require_device_f32("x", x)
+    _require_device_f32("flow12", flow)
+    B, C, H, W = _nchw("x", x)
+    if pad not in PAD_MODES:
+        raise NotImplementedError(f"flow_warp padding mode {pad!r} (supported: border, zeros)")
+    if flow.device != x.device:
+        raise ValueError("x and flow12 are on different devices")
+    xc = x.contiguous()
+    fv, fbs = _flow_view(flow, B, H, W)
+    out = torch.empty_like(xc)
+    lib = _lib.load()
+    with torch.cuda.device(x.device):
+        rc = lib.usf_warp_fwd_f32(
+            xc.data_ptr(), fv.data_ptr(), fbs, out.data_ptr(), B, C, H, W, PAD_MODES[pad],
+            _lib.stream_handle(x.device),
+        )
+    _lib.check(rc, "usf_warp_fwd_f32")
+    return out
+
+
+def warp_backward(
+    x: torch.Tensor,
+    flow: torch.Tensor,
+    grad_out: torch.Tensor,
+    pad: str = "border",
+    need_x: bool = True,
+    need_flow: bool = True,
+) -> tuple[torch.Tensor | None, torch.Tensor | None]:
+    """(grad_x, grad_flow) of :func:`warp_forward`. grad_x uses fp32 atomics."""
+    _require_device_f32("x", x)
+    _require_device_f32("flow12", flow)
+    _require_device_f32("grad_output", grad_out)
+    B, C, H, W = _nchw("x", x)
+    if pad not in PAD_MODES:
+        raise NotImplementedError(f"flow_warp padding mode {pad!r} (supported: border, zeros)")
+    if tuple(grad_out.shape) != (B, C, H, W):
+        raise ValueError(f"grad_output shape {tuple(grad_out.shape)} != {(B, C, H, W)}")
+    if not (need_x or need_flow):
+        return None, None
+    xc = x.contiguous()
+    fv, fbs = _flow_view(flow, B, H, W)
+    gc = grad_out.contiguous()
+    gx = torch.zeros_like(xc) if need_x else None
+    gf = torch.empty((B, 2, H, W), device=x.device, dtype=torch.float32) if need_flow else None
+    lib = _lib.load()
+    with torch.cuda.device(x.device):
+        rc = lib.usf_warp_bwd_f32(
+            xc.data_ptr(), fv.data_ptr(), fbs, gc.data_ptr(), _ptr(gx), _ptr(gf),
+            B, C, H, W, PAD_MODES[pad], _lib.stream_handle(x.device),
+        )
+    _lib.check(rc, "usf_warp_bwd_f32")
+    return gx, gf
