@@ -1,0 +1,229 @@
+#!/usr/bin/env python3
+"""Benchmark: image-pairs/sec of one PWCLite training step, KITTI 832x256, d=4.
+
+A step (unsamflow_amd.harness.TrainStep) is the reference trainer's step:
+PWCLite fwd with_bk (10 correlation + 8 decoder-warp calls through the HIP
+library) -> unFlowLoss (8 loss warps) -> backward -> clip_grad_norm_ -> Adam ->
+OneCycleLR, on B=8 synthetic U[0,1) frame pairs per GPU (kitti_base.json),
+random-init weights. N>1: one process per GPU (torchrun), DDP over RCCL
+("nccl"), B=8 per rank (weak scaling).
+
+Output: ONE JSON line on rank 0 with the driver's contract fields plus
+* ``roofline`` — the dominant hot-path kernel (largest summed time per step):
+  algorithmic bytes per launch / its mean duration, measured
+  with HIP events on the launch stream in an instrumented pass of real steps
+  that follows the timed region;
+* ``levels`` — per call site (op, level shape) mean us, GB/s, HBM fraction;
+* ``cpu_baseline`` — the oracle's torch-CPU restatement of the same step
+  (correlation_native-style correlation + grid_sample warp) on the host cores,
+  rank 0 at N=1 only, bounded sample.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
+                       [--config kitti|sintel_mf] [--no-cpu-baseline]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+if REPO not in sys.path:
+    sys.path.insert(0, REPO)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+HBM_PEAK_GBPS = 8000.0  # MI355X spec (MI355X_MICROARCH.md); ~6300 measured copy
+CONFIGS = {
+    "kitti": dict(H=256, W=832, workload="PWCLite fwd(with_bk)+unFlowLoss+bwd+Adam, KITTI 832x256, d=4"),
+    "sintel_mf": dict(H=448, W=1024, workload="PWCLite+mask-feature corr fwd(with_bk)+unFlowLoss+bwd+Adam, Sintel 1024x448, d=4"),
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--batch", type=int, default=8, help="pairs per GPU (kitti_base.json train.batch_size)")
+    ap.add_argument("--config", choices=sorted(CONFIGS), default="kitti")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-steps", type=int, default=2)
+    ap.add_argument("--cpu-batch", type=int, default=2)
+    ap.add_argument("--profile-steps", type=int, default=3, help="instrumented steps for per-kernel timing")
+    return ap.parse_args()
+
+
+def cfg_for(name):
+    from unsamflow_amd.config import kitti_base, sintel_mf
+
+    return kitti_base() if name == "kitti" else sintel_mf()
+
+
+def kernel_report(summary):
+    """Per call-site rows + the dominant kernel (max summed time per step)."""
+    rows = []
+    per_op = {}
+    for (op, key), a in summary.items():
+        rows.append({
+            "op": op, "shape": list(key), "calls": a["n"], "mean_us": round(a["mean_us"], 2),
+            "bytes": a["bytes"], "gbps": round(a["gbps"], 1), "hbm_frac": round(a["gbps"] / HBM_PEAK_GBPS, 4),
+            "tflops": round(a["tflops"], 2),
+        })
+        per_op.setdefault(op, 0.0)
+        per_op[op] += a["total_us"]
+    dom = max(summary.items(), key=lambda kv: kv[1]["total_us"])
+    (op, key), a = dom
+    roof = {
+        "bound": "hbm",
+        "kernel": op,
+        "shape": list(key),
+        "achieved": round(a["gbps"], 1),
+        "peak": HBM_PEAK_GBPS,
+        "unit": "GB/s",
+        "frac": round(a["gbps"] / HBM_PEAK_GBPS, 4),
+        "bytes_per_launch": a["bytes"],
+        "mean_us": round(a["mean_us"], 3),
+        "traffic": None,
+    }
+    return rows, roof, {k: round(v, 1) for k, v in per_op.items()}
+
+
+def cpu_baseline(args, cfg_name):
+    """Oracle (torch-CPU restatement) PWCLite step on the host cores, bounded."""
+    from oracle.torch_ref import OracleCorrelation, oracle_flow_warp
+    from unsamflow_amd.harness import TrainStep, synthetic_pair
+
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        cores = os.cpu_count() or 1
+    cores = min(cores, int(os.environ.get("OMP_NUM_THREADS", cores)))
+    torch.set_num_threads(cores)
+    c = CONFIGS[cfg_name]
+    step = TrainStep(cfg_for(cfg_name), "cpu", corr_module=OracleCorrelation(4), warp_fn=oracle_flow_warp,
+                     fused_adam=False)
+    img1, img2, s1, s2 = synthetic_pair(args.cpu_batch, c["H"], c["W"], "cpu", with_seg=cfg_name != "kitti")
+    step(img1, img2, s1, s2)  # warmup
+    t0 = time.perf_counter()
+    for _ in range(args.cpu_steps):
+        step(img1, img2, s1, s2)
+    dt = time.perf_counter() - t0
+    model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            model = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), "")
+    except OSError:
+        pass
+    return {
+        "value": round(args.cpu_batch * args.cpu_steps / dt, 4),
+        "unit": "image-pairs/s",
+        "cores": cores,
+        "kind": "port",
+        "sample": f"{args.cpu_steps} steps x B={args.cpu_batch} ({c['W']}x{c['H']}) of the same train step on CPU "
+                  f"with the oracle restatement (oracle/torch_ref.py) for corr+warp, after 1 warmup step; "
+                  f"{dt:.1f} s; {model}",
+    }
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and rank == 0:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+    distributed = world > 1
+    torch.cuda.set_device(local_rank)
+    device = torch.device("cuda", local_rank)
+    if distributed:
+        dist.init_process_group("nccl", device_id=device)
+    torch.backends.cudnn.benchmark = True
+
+    from unsamflow_amd import _lib
+    from unsamflow_amd.harness import TrainStep, synthetic_pair
+    from unsamflow_amd.kernel_timer import KernelTimer
+
+    _lib.load()  # fail loudly if the HIP library is missing
+    c = CONFIGS[args.config]
+    cfg = cfg_for(args.config)
+    step = TrainStep(cfg, device, ddp=distributed, seed=42 + rank)
+    img1, img2, s1, s2 = synthetic_pair(args.batch, c["H"], c["W"], device, seed=42 + rank,
+                                        with_seg=args.config != "kitti")
+
+    for i in range(args.warmup):
+        step(img1, img2, s1, s2)
+    torch.cuda.synchronize()
+
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step(img1, img2, s1, s2)
+    torch.cuda.synchronize()
+    if distributed:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if distributed:
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    loss_val = float(loss.item())
+
+    # instrumented pass: per-launch HIP events around every hot-path kernel
+    with KernelTimer() as kt:
+        for _ in range(args.profile_steps):
+            step(img1, img2, s1, s2)
+    torch.cuda.synchronize()
+    summary = kt.summary()
+    for a in summary.values():  # calls per step
+        a["n_per_step"] = a["n"] / max(1, args.profile_steps)
+    rows, roof, per_op_us = kernel_report(summary)
+    per_op_us = {k: round(v / max(1, args.profile_steps), 1) for k, v in per_op_us.items()}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args, args.config)
+
+    if rank == 0:
+        pairs = args.batch * world * args.steps
+        value = pairs / elapsed
+        out = {
+            "metric": "image-pairs/sec PWCLite fwd+bwd, KITTI 832x256 d=4" if args.config == "kitti"
+            else "image-pairs/sec PWCLite+mask-corr fwd+bwd, Sintel 1024x448 d=4",
+            "value": round(value, 3),
+            "unit": "image-pairs/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic U[0,1) frame pairs, random-init PWCLite weights",
+            "config": {
+                "workload": c["workload"],
+                "global_batch": args.batch * world,
+                "per_gpu_batch": args.batch,
+                "image_hw": [c["H"], c["W"]],
+                "max_displacement": 4,
+                "parallelism": f"dp{world}",
+            },
+            "roofline": roof,
+            "cpu_baseline": cpu,
+            "hot_path_us_per_step": per_op_us,
+            "levels": rows,
+            "final_loss": round(loss_val, 6),
+        }
+        print(json.dumps(out), flush=True)
+    if distributed:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,132 @@
+"""Training-step harness around the hot path (the benchmark's "step").
+
+Reproduces the shape of the reference's training step
+(trainer/kitti_trainer_ar.py:108-317 with trainer/base_trainer.py:141-169):
+
+    res = model(img1, img2, with_bk=True)
+    flows = [cat(f12, f21)]                       # :113-117
+    loss = unFlowLoss(flows, img1, img2).mean()   # :127-133
+    optimizer.zero_grad(set_to_none=True); loss.backward()          # :309-310
+    clip_grad_norm_(params, max_grad_norm); optimizer.step(); scheduler.step()  # :313-317
+
+with Adam(betas=(momentum, beta), eps=1e-7) over the bias / weight parameter
+groups (base_trainer.py:141-169) and OneCycleLR. Data is synthetic (U[0,1)
+frames, as ``/255`` images of datasets/flow_datasets.py:59-63). With
+``ddp=True`` the model is wrapped in DistributedDataParallel (train.py:116-120):
+one process per GPU, gradient all-reduce over RCCL ("nccl" backend) / gloo.
+
+The per-step host syncs of the reference's logging (``loss.item()``,
+kitti_trainer_ar.py:284-293) are not part of the step.
+"""
+from __future__ import annotations
+
+from typing import Callable
+
+import torch
+
+from .flow_loss import unFlowLoss
+from .pwclite import PWCLite
+
+
+def param_groups(model: torch.nn.Module, train_cfg) -> list[dict]:
+    """Bias / weight / other groups as utils/torch_utils.py:27-40 (empty groups dropped)."""
+    named = list(model.named_parameters())
+    groups = [
+        {"params": [p for n, p in named if ".bias" in n], "weight_decay": train_cfg.bias_decay},
+        {"params": [p for n, p in named if ".weight" in n], "weight_decay": train_cfg.weight_decay},
+        {"params": [p for n, p in named if ".bias" not in n and ".weight" not in n], "weight_decay": 0},
+    ]
+    return [g for g in groups if g["params"]]
+
+
+def synthetic_pair(B: int, H: int, W: int, device, seed: int = 42, with_seg: bool = False, n_seg: int = 32):
+    """U[0,1) frame pair [B,3,H,W] (+ piecewise-constant segment maps [B,1,H,W] as float)."""
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    img1 = torch.rand(B, 3, H, W, generator=g).to(device)
+    img2 = torch.rand(B, 3, H, W, generator=g).to(device)
+    if not with_seg:
+        return img1, img2, None, None
+    blk = 32
+    segs = []
+    for _ in range(2):
+        ids = torch.randint(0, n_seg, (B, 1, (H + blk - 1) // blk, (W + blk - 1) // blk), generator=g).float()
+        seg = ids.repeat_interleave(blk, 2).repeat_interleave(blk, 3)[:, :, :H, :W]
+        segs.append(seg.contiguous().to(device))
+    return img1, img2, segs[0], segs[1]
+
+
+class TrainStep:
+    """One PWCLite fwd(with_bk) + unFlowLoss + bwd + clip + Adam + OneCycleLR step."""
+
+    def __init__(self, cfg, device, ddp: bool = False, corr_module=None, warp_fn: Callable | None = None,
+                 loss_kwargs: dict | None = None, fused_adam: bool | None = None, seed: int = 42):
+        torch.manual_seed(seed)
+        self.cfg = cfg
+        self.device = torch.device(device)
+        model = PWCLite(cfg.model, corr_module=corr_module, warp_fn=warp_fn).to(self.device)
+        self.module = model
+        if ddp:
+            ids = [self.device.index] if self.device.type == "cuda" else None
+            model = torch.nn.parallel.DistributedDataParallel(model, device_ids=ids)
+        self.model = model
+        self.loss_fn = unFlowLoss(cfg.loss, warp_fn=warp_fn, **(loss_kwargs or {}))
+        t = cfg.train
+        if fused_adam is None:
+            fused_adam = self.device.type == "cuda"
+        self.optimizer = torch.optim.Adam(param_groups(self.module, t), t.lr, betas=(t.momentum, t.beta), eps=1e-7,
+                                          fused=fused_adam or None)
+        sched = t.get("lr_scheduler")
+        if sched and sched.module == "OneCycleLR":
+            p = dict(sched.params)
+            p.update(epochs=t.epoch_num, steps_per_epoch=t.epoch_size)
+            self.scheduler = torch.optim.lr_scheduler.OneCycleLR(self.optimizer, **p)
+        else:
+            self.scheduler = torch.optim.lr_scheduler.ExponentialLR(self.optimizer, gamma=1)
+        self.max_grad_norm = t.max_grad_norm
+
+    def forward_loss(self, img1, img2, full_seg1=None, full_seg2=None):
+        res = self.model(img1, img2, full_seg1, full_seg2, with_bk=True)
+        flows = [torch.cat([a, b], 1) for a, b in zip(res["flows_12"], res["flows_21"])]
+        kw = {}
+        if full_seg1 is not None:
+            kw = dict(full_seg1=full_seg1, full_seg2=full_seg2)
+        loss, l_ph, l_sm, fmean, _, _ = self.loss_fn(flows, img1, img2, **kw)
+        return loss.mean(), flows
+
+    def __call__(self, img1, img2, full_seg1=None, full_seg2=None):
+        loss, _ = self.forward_loss(img1, img2, full_seg1, full_seg2)
+        self.optimizer.zero_grad(set_to_none=True)
+        loss.backward()
+        torch.nn.utils.clip_grad_norm_(self.model.parameters(), self.max_grad_norm)
+        self.optimizer.step()
+        self.scheduler.step()
+        return loss.detach()
+
+
+def smoke_step(device) -> None:
+    """Tiny PWCLite step on ``device`` checked against the same model on CPU with
+    the oracle ops (hash-initialised weights, 64x128, B=1)."""
+    from oracle.hashrng import hash_init_, uniform
+    from oracle.torch_ref import OracleCorrelation, oracle_flow_warp
+
+    from .config import kitti_base
+
+    cfg = kitti_base()
+    gpu = TrainStep(cfg, device)
+    cpu = TrainStep(kitti_base(), "cpu", corr_module=OracleCorrelation(4), warp_fn=oracle_flow_warp)
+    hash_init_(gpu.module, seed=1)
+    hash_init_(cpu.module, seed=1)
+    im1 = torch.from_numpy(uniform((1, 3, 64, 128), 11))
+    im2 = torch.from_numpy(uniform((1, 3, 64, 128), 12))
+    lg, fg = gpu.forward_loss(im1.to(device), im2.to(device))
+    lc, fc = cpu.forward_loss(im1, im2)
+    lg.backward()
+    lc.backward()
+    torch.cuda.synchronize(device)
+    assert torch.isfinite(lg), lg
+    assert abs(lg.item() - lc.item()) <= 1e-4 * abs(lc.item()) + 1e-6, (lg.item(), lc.item())
+    torch.testing.assert_close(fg[0].cpu(), fc[0].detach(), atol=2e-4, rtol=1e-3)
+    for (n, pg), pc in zip(gpu.module.named_parameters(), cpu.module.parameters()):
+        torch.testing.assert_close(pg.grad.cpu(), pc.grad, atol=1e-4, rtol=5e-3, msg=n)
+    step = gpu(im1.to(device), im2.to(device))
+    assert torch.isfinite(step)

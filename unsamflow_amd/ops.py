@@ -10,6 +10,7 @@ from __future__ import annotations
 import torch
 
 from . import _lib
+from . import kernel_timer as _kt
 
 PAD_MODES = {"zeros": _lib.PAD_ZEROS, "border": _lib.PAD_BORDER}
 
@@ -50,7 +51,9 @@ def corr_forward(x1: torch.Tensor, x2: torch.Tensor, max_displacement: int) -> t
     x1c, x2c = x1.contiguous(), x2.contiguous()
     out = torch.empty((B, K * K, H, W), device=x1.device, dtype=torch.float32)
     lib = _lib.load()
-    with torch.cuda.device(x1.device):
+    with torch.cuda.device(x1.device), _kt.timed(
+        "corr_fwd", (B, C, H, W), x1.device, _kt.corr_bytes(B, C, H, W, K * K), _kt.corr_flops(B, C, H, W, K * K)
+    ):
         rc = lib.usf_corr_fwd_f32(
             x1c.data_ptr(), x2c.data_ptr(), out.data_ptr(), B, C, H, W, d, _lib.stream_handle(x1.device)
         )
@@ -81,7 +84,11 @@ def corr_backward(
     g1 = torch.empty_like(x1c) if need_x1 else None
     g2 = torch.empty_like(x2c) if need_x2 else None
     lib = _lib.load()
-    with torch.cuda.device(x1.device):
+    with torch.cuda.device(x1.device), _kt.timed(
+        "corr_bwd", (B, C, H, W, need_x1, need_x2), x1.device,
+        _kt.corr_bytes(B, C, H, W, K * K, True, need_x1, need_x2),
+        _kt.corr_flops(B, C, H, W, K * K, True, need_x1, need_x2),
+    ):
         rc = lib.usf_corr_bwd_f32(
             x1c.data_ptr(), x2c.data_ptr(), gc.data_ptr(), _ptr(g1), _ptr(g2),
             B, C, H, W, d, _lib.stream_handle(x1.device),
@@ -118,7 +125,7 @@ def warp_forward(x: torch.Tensor, flow: torch.Tensor, pad: str = "border") -> to
     fv, fbs = _flow_view(flow, B, H, W)
     out = torch.empty_like(xc)
     lib = _lib.load()
-    with torch.cuda.device(x.device):
+    with torch.cuda.device(x.device), _kt.timed("warp_fwd", (B, C, H, W, pad), x.device, _kt.warp_bytes(B, C, H, W)):
         rc = lib.usf_warp_fwd_f32(
             xc.data_ptr(), fv.data_ptr(), fbs, out.data_ptr(), B, C, H, W, PAD_MODES[pad],
             _lib.stream_handle(x.device),
@@ -152,7 +159,10 @@ def warp_backward(
     gx = torch.zeros_like(xc) if need_x else None
     gf = torch.empty((B, 2, H, W), device=x.device, dtype=torch.float32) if need_flow else None
     lib = _lib.load()
-    with torch.cuda.device(x.device):
+    with torch.cuda.device(x.device), _kt.timed(
+        "warp_bwd", (B, C, H, W, pad, need_x, need_flow), x.device,
+        _kt.warp_bytes(B, C, H, W, True, need_x, need_flow),
+    ):
         rc = lib.usf_warp_bwd_f32(
             xc.data_ptr(), fv.data_ptr(), fbs, gc.data_ptr(), _ptr(gx), _ptr(gf),
             B, C, H, W, PAD_MODES[pad], _lib.stream_handle(x.device),
