@@ -51,9 +51,11 @@ def parse():
     ap.add_argument("--batch", type=int, default=8, help="pairs per GPU (kitti_base.json train.batch_size)")
     ap.add_argument("--config", choices=sorted(CONFIGS), default="kitti")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-steps", type=int, default=2)
-    ap.add_argument("--cpu-batch", type=int, default=2)
+    ap.add_argument("--cpu-steps", type=int, default=6)
+    ap.add_argument("--cpu-batch", type=int, default=4)
     ap.add_argument("--profile-steps", type=int, default=3, help="instrumented steps for per-kernel timing")
+    ap.add_argument("--cudnn-benchmark", action="store_true",
+                    help="MIOpen find-mode tuning of the convolutions (slow first steps)")
     return ap.parse_args()
 
 
@@ -63,31 +65,40 @@ def cfg_for(name):
     return kitti_base() if name == "kitti" else sintel_mf()
 
 
-def kernel_report(summary):
-    """Per call-site rows + the dominant kernel (max summed time per step)."""
-    rows = []
-    per_op = {}
-    for (op, key), a in summary.items():
-        rows.append({
-            "op": op, "shape": list(key), "calls": a["n"], "mean_us": round(a["mean_us"], 2),
-            "bytes": a["bytes"], "gbps": round(a["gbps"], 1), "hbm_frac": round(a["gbps"] / HBM_PEAK_GBPS, 4),
-            "tflops": round(a["tflops"], 2),
-        })
-        per_op.setdefault(op, 0.0)
-        per_op[op] += a["total_us"]
-    dom = max(summary.items(), key=lambda kv: kv[1]["total_us"])
-    (op, key), a = dom
+def kernel_report(summary, device, steps):
+    """Per call site: in-step (event-bracketed) time, device time (graph replay),
+    algorithmic GB/s and HBM fraction; plus the dominant kernel's roofline."""
+    from unsamflow_amd.kernel_timer import device_time_us, site_launcher
+
+    rows, per_op = [], {}
+    best = None
+    for i, ((op, key), a) in enumerate(summary.items()):
+        dev_us = device_time_us(site_launcher(op, key, device, seed=i))
+        calls = a["n"] / max(1, steps)
+        gbps = a["bytes"] / (dev_us * 1e-6) / 1e9
+        row = {
+            "op": op, "shape": list(key), "calls_per_step": calls, "device_us": round(dev_us, 2),
+            "in_step_us": round(a["mean_us"], 2), "bytes": a["bytes"], "gbps": round(gbps, 1),
+            "hbm_frac": round(gbps / HBM_PEAK_GBPS, 4),
+            "tflops": round(a["flops"] / (dev_us * 1e-6) / 1e12, 2),
+        }
+        rows.append(row)
+        per_op[op] = per_op.get(op, 0.0) + calls * dev_us
+        if best is None or calls * dev_us > best[0]:
+            best = (calls * dev_us, row)
+    row = best[1]
     roof = {
         "bound": "hbm",
-        "kernel": op,
-        "shape": list(key),
-        "achieved": round(a["gbps"], 1),
+        "kernel": row["op"],
+        "shape": row["shape"],
+        "achieved": row["gbps"],
         "peak": HBM_PEAK_GBPS,
         "unit": "GB/s",
-        "frac": round(a["gbps"] / HBM_PEAK_GBPS, 4),
-        "bytes_per_launch": a["bytes"],
-        "mean_us": round(a["mean_us"], 3),
+        "frac": row["hbm_frac"],
+        "bytes_per_launch": row["bytes"],
+        "mean_us": row["device_us"],
         "traffic": None,
+        "method": "algorithmic bytes (SURVEY 8d) / device time of 20 graph-replayed launches (HIP events)",
     }
     return rows, roof, {k: round(v, 1) for k, v in per_op.items()}
 
@@ -141,7 +152,7 @@ def main():
     device = torch.device("cuda", local_rank)
     if distributed:
         dist.init_process_group("nccl", device_id=device)
-    torch.backends.cudnn.benchmark = True
+    torch.backends.cudnn.benchmark = bool(args.cudnn_benchmark)
 
     from unsamflow_amd import _lib
     from unsamflow_amd.harness import TrainStep, synthetic_pair
@@ -180,10 +191,7 @@ def main():
             step(img1, img2, s1, s2)
     torch.cuda.synchronize()
     summary = kt.summary()
-    for a in summary.values():  # calls per step
-        a["n_per_step"] = a["n"] / max(1, args.profile_steps)
-    rows, roof, per_op_us = kernel_report(summary)
-    per_op_us = {k: round(v / max(1, args.profile_steps), 1) for k, v in per_op_us.items()}
+    rows, roof, per_op_us = kernel_report(summary, device, args.profile_steps)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -216,7 +224,7 @@ def main():
             },
             "roofline": roof,
             "cpu_baseline": cpu,
-            "hot_path_us_per_step": per_op_us,
+            "hot_path_device_us_per_step": per_op_us,
             "levels": rows,
             "final_loss": round(loss_val, 6),
         }

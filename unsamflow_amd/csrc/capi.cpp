@@ -5,6 +5,7 @@
 #include <climits>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 
 #include "../../include/unsamflow_hip.h"
 #include "usf_common.h"
@@ -36,7 +37,34 @@ static bool check_dims(const char* fn, int B, int C, int H, int W) {
   return true;
 }
 
-static int finish(const char* fn, hipError_t e) {
+// USF_SYNC_CHECK=1: synchronise the stream after every launch and report any
+// asynchronous fault against the launch that caused it (debug only).
+static bool sync_check() {
+  static const bool on = [] {
+    const char* v = getenv("USF_SYNC_CHECK");
+    return v && v[0] == '1';
+  }();
+  return on;
+}
+
+// With USF_SYNC_CHECK=1 every entry point first drains the stream, so a fault
+// raised by an EARLIER (non-usf) kernel is reported as such, not blamed on us.
+static int pre_check(const char* fn, hipStream_t s) {
+  if (!sync_check()) return 0;
+  const hipError_t e = hipStreamSynchronize(s);
+  if (e != hipSuccess) {
+    fprintf(stderr, "[usf] %s: stream already faulted BEFORE this launch: %s\n", fn, hipGetErrorString(e));
+    set_error("%s: stream faulted before launch: %s (%d)", fn, hipGetErrorString(e), (int)e);
+    return (int)e;
+  }
+  return 0;
+}
+
+static int finish(const char* fn, hipError_t e, hipStream_t s) {
+  if (e == hipSuccess && sync_check()) {
+    e = hipStreamSynchronize(s);
+    if (e != hipSuccess) fprintf(stderr, "[usf] %s: fault after launch: %s\n", fn, hipGetErrorString(e));
+  }
   if (e != hipSuccess) {
     set_error("%s: HIP launch failed: %s (%d)", fn, hipGetErrorString(e), (int)e);
     return (int)e;
@@ -66,8 +94,9 @@ int usf_corr_fwd_f32(const float* x1, const float* x2, float* out, int B, int C,
     set_error("usf_corr_fwd_f32: null pointer");
     return USF_EINVAL;
   }
+  if (const int pe = pre_check("usf_corr_fwd_f32", (hipStream_t)stream)) return pe;
   return finish("usf_corr_fwd_f32",
-                corr_fwd_launch(x1, x2, out, B, C, H, W, d, (hipStream_t)stream));
+                corr_fwd_launch(x1, x2, out, B, C, H, W, d, (hipStream_t)stream), (hipStream_t)stream);
 }
 
 int usf_corr_bwd_f32(const float* x1, const float* x2, const float* gout, float* gx1,
@@ -82,8 +111,10 @@ int usf_corr_bwd_f32(const float* x1, const float* x2, const float* gout, float*
     set_error("usf_corr_bwd_f32: null input pointer");
     return USF_EINVAL;
   }
+  if (const int pe = pre_check("usf_corr_bwd_f32", (hipStream_t)stream)) return pe;
   return finish("usf_corr_bwd_f32",
-                corr_bwd_launch(x1, x2, gout, gx1, gx2, B, C, H, W, d, (hipStream_t)stream));
+                corr_bwd_launch(x1, x2, gout, gx1, gx2, B, C, H, W, d, (hipStream_t)stream),
+                (hipStream_t)stream);
 }
 
 int usf_warp_fwd_f32(const float* x, const float* flow, long long flow_bstride, float* out,
@@ -102,8 +133,10 @@ int usf_warp_fwd_f32(const float* x, const float* flow, long long flow_bstride, 
     set_error("usf_warp_fwd_f32: flow batch stride %lld < 2*H*W", flow_bstride);
     return USF_EINVAL;
   }
-  return finish("usf_warp_fwd_f32", warp_fwd_launch(x, flow, flow_bstride, out, B, C, H, W,
-                                                    pad_mode, (hipStream_t)stream));
+  if (const int pe = pre_check("usf_warp_fwd_f32", (hipStream_t)stream)) return pe;
+  return finish("usf_warp_fwd_f32",
+                warp_fwd_launch(x, flow, flow_bstride, out, B, C, H, W, pad_mode, (hipStream_t)stream),
+                (hipStream_t)stream);
 }
 
 int usf_warp_bwd_f32(const float* x, const float* flow, long long flow_bstride,
@@ -123,8 +156,11 @@ int usf_warp_bwd_f32(const float* x, const float* flow, long long flow_bstride,
     set_error("usf_warp_bwd_f32: flow batch stride %lld < 2*H*W", flow_bstride);
     return USF_EINVAL;
   }
-  return finish("usf_warp_bwd_f32", warp_bwd_launch(x, flow, flow_bstride, gout, gx, gflow, B,
-                                                    C, H, W, pad_mode, (hipStream_t)stream));
+  if (const int pe = pre_check("usf_warp_bwd_f32", (hipStream_t)stream)) return pe;
+  return finish("usf_warp_bwd_f32",
+                warp_bwd_launch(x, flow, flow_bstride, gout, gx, gflow, B, C, H, W, pad_mode,
+                                (hipStream_t)stream),
+                (hipStream_t)stream);
 }
 
 }  // extern "C"

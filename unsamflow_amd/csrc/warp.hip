@@ -36,6 +36,12 @@ struct Tap {
 
 __device__ __forceinline__ Tap make_tap(float u, float v, int x, int y, int H, int W,
                                         bool border) {
+  // Every step of the coordinate chain is rounded separately, as in the
+  // reference: hipcc's default -ffp-contract=fast would otherwise fuse
+  // w = ix - floor(ix) into fma(sx, gx+1, -floor) on the unrounded product,
+  // which moves the sample point by up to 1 ulp of the coordinate (6e-5 px
+  // at W=832) and the output by ~3e-5.
+#pragma clang fp contract(off)
   Tap t;
   const float wm1 = (float)(W - 1), hm1 = (float)(H - 1);
   // norm_grid: 2.0 * v / (W - 1) - 1.0  (fp32, true division as in torch CPU)
@@ -81,10 +87,9 @@ __global__ __launch_bounds__(256) void warp_fwd_kernel(const float* __restrict__
                                                        long long fbs, float* __restrict__ out,
                                                        int B, int C, int H, int W) {
   const int HW = H * W;
-  const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (idx >= (long long)B * HW) return;
-  const int b = (int)(idx / HW);
-  const int p = (int)(idx - (long long)b * HW);
+  const int p = blockIdx.x * 256 + threadIdx.x;  // pixel within the sample
+  const int b = blockIdx.y;
+  if (p >= HW) return;
   const int y = p / W, xx = p - y * W;
   const float* fb = flow + b * fbs;
   const Tap t = make_tap(fb[p], fb[HW + p], xx, y, H, W, BORDER);
@@ -111,10 +116,9 @@ __global__ __launch_bounds__(256) void warp_bwd_kernel(const float* __restrict__
                                                        float* __restrict__ gflow, int B, int C,
                                                        int H, int W) {
   const int HW = H * W;
-  const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (idx >= (long long)B * HW) return;
-  const int b = (int)(idx / HW);
-  const int p = (int)(idx - (long long)b * HW);
+  const int p = blockIdx.x * 256 + threadIdx.x;
+  const int b = blockIdx.y;
+  if (p >= HW) return;
   const int y = p / W, xx = p - y * W;
   const float* fb = flow + b * fbs;
   const Tap t = make_tap(fb[p], fb[HW + p], xx, y, H, W, BORDER);
@@ -155,8 +159,7 @@ __global__ __launch_bounds__(256) void warp_bwd_kernel(const float* __restrict__
 template <bool BORDER>
 hipError_t bwd_launch_pad(const float* x, const float* flow, long long fbs, const float* gout,
                           float* gx, float* gflow, int B, int C, int H, int W, hipStream_t s) {
-  const long long n = (long long)B * H * W;
-  const dim3 grid((unsigned)((n + 255) / 256)), block(256);
+  const dim3 grid((unsigned)((H * W + 255) / 256), (unsigned)B), block(256);
   if (gx && gflow)
     hipLaunchKernelGGL((warp_bwd_kernel<BORDER, true, true>), grid, block, 0, s, x, flow, fbs,
                        gout, gx, gflow, B, C, H, W);
@@ -173,8 +176,7 @@ hipError_t bwd_launch_pad(const float* x, const float* flow, long long fbs, cons
 
 hipError_t warp_fwd_launch(const float* x, const float* flow, long long fbs, float* out, int B,
                            int C, int H, int W, int pad_mode, hipStream_t s) {
-  const long long n = (long long)B * H * W;
-  const dim3 grid((unsigned)((n + 255) / 256)), block(256);
+  const dim3 grid((unsigned)((H * W + 255) / 256), (unsigned)B), block(256);
   if (pad_mode == 1)
     hipLaunchKernelGGL((warp_fwd_kernel<true>), grid, block, 0, s, x, flow, fbs, out, B, C, H, W);
   else

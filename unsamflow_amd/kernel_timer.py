@@ -1,12 +1,21 @@
-"""Optional per-launch timing of the HIP hot-path kernels with HIP events.
+"""Per-call-site timing of the HIP hot-path kernels.
 
-When enabled (``with KernelTimer() as kt: ...``), every launch made through
-:mod:`unsamflow_amd.ops` is bracketed by two ``torch.cuda.Event`` records on
-the stream the kernel is launched on (torch's current stream of the tensor's
-device — the same stream ops.py passes to the library), tagged with the op
-name, shape and the algorithmic byte / flop counts of SURVEY.md §8d. After a
-device sync, :meth:`KernelTimer.summary` aggregates mean duration and
-achieved GB/s per (op, shape). Disabled, it costs one global check per call.
+Two measurements, both with HIP events on the stream the kernels are launched
+on (torch's current stream — the stream ops.py hands to the library):
+
+* ``KernelTimer`` — while active, every launch made through
+  :mod:`unsamflow_amd.ops` is bracketed by two event records inside the real
+  training step and its call site (op, shape, flags) is recorded. These
+  in-step intervals include any time the GPU waits for the host to enqueue
+  the kernel, so they bound the kernel time from above.
+* ``device_time_us`` — the kernel's device time: REPS launches of one call
+  site captured into a HIP graph, replayed back to back between two events,
+  divided by the launch count. No host gaps; this is what ``roofline`` uses and
+  what ``rocprofv3 --kernel-trace --stats`` reports as the average duration.
+
+Algorithmic bytes / flops per launch follow SURVEY.md §8(d): every input read
+once, every output written once (halo re-reads, scratch and zero-fill
+excluded).
 """
 from __future__ import annotations
 
@@ -21,8 +30,7 @@ _active: "KernelTimer | None" = None
 def corr_bytes(B, C, H, W, K2=81, backward=False, need1=True, need2=True):
     if not backward:
         return 4 * B * H * W * (2 * C + K2)
-    # read g once, read the x each grad needs, write each grad once
-    n = int(need1) + int(need2)
+    n = int(need1) + int(need2)  # read g once, read x_j and write grad_i per needed grad
     return 4 * B * H * W * (K2 + 2 * n * C)
 
 
@@ -34,17 +42,17 @@ def corr_flops(B, C, H, W, K2=81, backward=False, need1=True, need2=True):
 def warp_bytes(B, C, H, W, backward=False, need_x=True, need_flow=True):
     if not backward:
         return 4 * B * H * W * (2 * C + 2)
-    per_px = 2  # read flow
-    per_px += C  # read grad_out
+    per_px = 2 + C  # flow, grad_out
     if need_flow:
-        per_px += C + 2  # read x, write grad_flow
+        per_px += C + 2  # x, grad_flow
     if need_x:
-        per_px += C  # grad_x (read-modify-write by atomics counted once)
+        per_px += C  # grad_x
     return 4 * B * H * W * per_px
 
 
 class KernelTimer:
-    def __init__(self):
+    def __init__(self, time_in_step: bool = True):
+        self.time_in_step = time_in_step
         self.records = []  # (op, key, start_event, end_event, bytes, flops)
 
     def __enter__(self):
@@ -59,17 +67,15 @@ class KernelTimer:
         return False
 
     def summary(self):
-        """{(op, key): dict(n, mean_us, bytes, flops, gbps, tflops)} — call after a device sync."""
+        """{(op, key): dict(n, mean_us (in-step), bytes, flops)} — call after a device sync."""
         agg = collections.OrderedDict()
         for op, key, s, e, nbytes, flops in self.records:
-            ms = s.elapsed_time(e)
             a = agg.setdefault((op, key), {"n": 0, "total_us": 0.0, "bytes": nbytes, "flops": flops})
             a["n"] += 1
-            a["total_us"] += ms * 1e3
+            if s is not None:
+                a["total_us"] += s.elapsed_time(e) * 1e3
         for a in agg.values():
             a["mean_us"] = a["total_us"] / a["n"]
-            a["gbps"] = a["bytes"] / (a["mean_us"] * 1e-6) / 1e9
-            a["tflops"] = a["flops"] / (a["mean_us"] * 1e-6) / 1e12
         return agg
 
 
@@ -80,6 +86,10 @@ def timed(op: str, key, device, nbytes: int, flops: int = 0):
     if kt is None:
         yield
         return
+    if not kt.time_in_step:
+        yield
+        kt.records.append((op, key, None, None, nbytes, flops))
+        return
     s = torch.cuda.Event(enable_timing=True)
     e = torch.cuda.Event(enable_timing=True)
     stream = torch.cuda.current_stream(device)
@@ -87,3 +97,58 @@ def timed(op: str, key, device, nbytes: int, flops: int = 0):
     yield
     e.record(stream)
     kt.records.append((op, key, s, e, nbytes, flops))
+
+
+def site_launcher(op: str, key, device, seed: int = 0):
+    """A closure launching one kernel of call site (op, key) on synthetic inputs.
+
+    Inputs: N(0,1) features / gradients; warp flows U[-2,2) px (the magnitude
+    of the decoder's and loss's flows early in training) and U[0,1) images.
+    """
+    from . import ops
+
+    g = torch.Generator(device=device).manual_seed(seed)
+    if op in ("corr_fwd", "corr_bwd"):
+        B, C, H, W = key[:4]
+        x1 = torch.randn(B, C, H, W, device=device, generator=g)
+        x2 = torch.randn(B, C, H, W, device=device, generator=g)
+        if op == "corr_fwd":
+            return lambda: ops.corr_forward(x1, x2, 4)
+        need1, need2 = key[4], key[5]
+        go = torch.randn(B, 81, H, W, device=device, generator=g)
+        return lambda: ops.corr_backward(x1, x2, go, 4, need1, need2)
+    B, C, H, W, pad = key[:5]
+    x = torch.rand(B, C, H, W, device=device, generator=g)
+    flow = (torch.rand(B, 2, H, W, device=device, generator=g) - 0.5) * 4
+    if op == "warp_fwd":
+        return lambda: ops.warp_forward(x, flow, pad)
+    need_x, need_flow = key[5], key[6]
+    go = torch.randn(B, C, H, W, device=device, generator=g)
+    return lambda: ops.warp_backward(x, flow, go, pad, need_x, need_flow)
+
+
+def device_time_us(fn, reps: int = 20, iters: int = 5) -> float:
+    """Mean device time of one ``fn()`` launch: REPS launches in a HIP graph, replayed."""
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        for _ in range(3):
+            fn()
+    torch.cuda.current_stream().wait_stream(side)
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        for _ in range(reps):
+            fn()
+    graph.replay()
+    torch.cuda.synchronize()
+    s = torch.cuda.Event(enable_timing=True)
+    e = torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        graph.replay()
+    e.record()
+    e.synchronize()
+    us = s.elapsed_time(e) * 1e3 / (iters * reps)
+    del graph
+    return us
