@@ -219,7 +219,10 @@ def test_warp_fwd_bwd_vs_reference_golden(hip_device, name):
 
 
 @pytest.mark.parametrize("pad", ["border", "zeros"])
-@pytest.mark.parametrize("shape,scale", [((8, 32, 64, 208), 3.0), ((2, 3, 256, 832), 40.0), ((4, 128, 8, 26), 1.5)])
+@pytest.mark.parametrize("shape,scale", [
+    ((8, 32, 64, 208), 3.0), ((2, 3, 256, 832), 40.0), ((4, 128, 8, 26), 1.5),
+    ((8, 64, 32, 104), 2.5), ((2, 5, 9, 7), 3.0), ((1, 96, 16, 52), 8.0),
+])
 def test_warp_vs_oracle_call_site_shapes(hip_device, pad, shape, scale):
     from unsamflow_amd import ops
 

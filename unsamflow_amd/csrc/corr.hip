@@ -45,12 +45,21 @@ struct FwdCfg {
   static constexpr int C2 = TW + 2 * D;         // staged x2 cols
   static constexpr int WIN = round_up(PX + 2 * D, 4);
   static constexpr int XS = round_up(C2, 4) + 4;  // LDS row stride (floats)
-  static constexpr int S1N = CC * TH * TW;
+  static constexpr int N1 = CC * TH * TW;         // staged x1 elements per stage
+  static constexpr int N2 = CC * R2 * C2;         // staged x2 elements per stage
+  static constexpr int L1 = (N1 + NT - 1) / NT;   // per-thread staging registers
+  static constexpr int L2 = (N2 + NT - 1) / NT;
+  static constexpr int S1N = N1;
   static constexpr int S2N = CC * R2 * XS + WIN;  // + tail pad for window over-read
   static_assert(PX % 4 == 0, "PX must be a multiple of 4 (ds_read_b128)");
   static_assert(64 % SEGX == 0, "SEGX must divide 64");
 };
 
+// Staging: every global load of a stage is issued before the first LDS write
+// (unconditional loads from clamped addresses, zero selected afterwards —
+// a per-element "load or 0" branch would make hipcc wait for each load in
+// turn), and the next stage's loads are in flight while the current stage is
+// computed (register double-buffering, one LDS image).
 template <int D, int PX, int SEGX, int NDY, int CC>
 __global__ __launch_bounds__(64 * NDY) void corr_fwd_kernel(const float* __restrict__ x1,
                                                             const float* __restrict__ x2,
@@ -58,7 +67,7 @@ __global__ __launch_bounds__(64 * NDY) void corr_fwd_kernel(const float* __restr
                                                             int H, int W, int tiles_x) {
   using F = FwdCfg<D, PX, SEGX, NDY, CC>;
   constexpr int K = F::K, TW = F::TW, TH = F::TH, NT = F::NT, R2 = F::R2, C2 = F::C2;
-  constexpr int WIN = F::WIN, XS = F::XS;
+  constexpr int WIN = F::WIN, XS = F::XS, N1 = F::N1, N2 = F::N2, L1 = F::L1, L2 = F::L2;
   __shared__ __attribute__((aligned(16))) float s1[F::S1N];
   __shared__ __attribute__((aligned(16))) float s2[F::S2N];
 
@@ -81,37 +90,58 @@ __global__ __launch_bounds__(64 * NDY) void corr_fwd_kernel(const float* __restr
   const int gy2 = y0 + dyb - D;  // image row of staged x2 row 0
   const int gx2 = x0 - D;        // image col of staged x2 col 0
 
+  float r1[L1], r2[L2];
+  auto fetch = [&](int c0) {
+#pragma unroll
+    for (int k = 0; k < L1; ++k) {
+      const int e = tid + k * NT;
+      const int c = e / (TH * TW);
+      const int rem = e - c * (TH * TW);
+      const int rr = rem / TW, cc = rem - (rem / TW) * TW;
+      const bool ok = e < N1 && c0 + c < C && y0 + rr < H && x0 + cc < W;
+      const float v = x1b[ok ? (c0 + c) * HW + (y0 + rr) * W + x0 + cc : 0];
+      r1[k] = ok ? v : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < L2; ++k) {
+      const int e = tid + k * NT;
+      const int c = e / (R2 * C2);
+      const int rem = e - c * (R2 * C2);
+      const int rr = rem / C2, cc = rem - (rem / C2) * C2;
+      const int gy = gy2 + rr, gx = gx2 + cc;
+      const bool ok = e < N2 && c0 + c < C && (unsigned)gy < (unsigned)H && (unsigned)gx < (unsigned)W;
+      const float v = x2b[ok ? (c0 + c) * HW + gy * W + gx : 0];
+      r2[k] = ok ? v : 0.f;
+    }
+  };
+  auto stash = [&]() {
+#pragma unroll
+    for (int k = 0; k < L1; ++k) {
+      const int e = tid + k * NT;
+      if (e < N1) s1[e] = r1[k];
+    }
+#pragma unroll
+    for (int k = 0; k < L2; ++k) {
+      const int e = tid + k * NT;
+      const int c = e / (R2 * C2);
+      const int rem = e - c * (R2 * C2);
+      const int rr = rem / C2, cc = rem - (rem / C2) * C2;
+      if (e < N2) s2[c * (R2 * XS) + rr * XS + cc] = r2[k];
+    }
+  };
+
   float acc[K][PX];
 #pragma unroll
   for (int j = 0; j < K; ++j)
 #pragma unroll
     for (int i = 0; i < PX; ++i) acc[j][i] = 0.f;
 
+  fetch(0);
+  stash();
+  __syncthreads();
   for (int c0 = 0; c0 < C; c0 += CC) {
-    // stage x1 tile [CC][TH][TW]
-    for (int e = tid; e < F::S1N; e += NT) {
-      const int c = e / (TH * TW);
-      const int rem = e - c * (TH * TW);
-      const int rr = rem / TW;
-      const int cc = rem - rr * TW;
-      const int gc = c0 + c, gy = y0 + rr, gx = x0 + cc;
-      float v = 0.f;
-      if (gc < C && gy < H && gx < W) v = x1b[gc * HW + gy * W + gx];
-      s1[e] = v;
-    }
-    // stage x2 halo [CC][R2][C2] (zero outside the image == the zero padding)
-    for (int e = tid; e < CC * R2 * C2; e += NT) {
-      const int c = e / (R2 * C2);
-      const int rem = e - c * (R2 * C2);
-      const int rr = rem / C2;
-      const int cc = rem - rr * C2;
-      const int gc = c0 + c, gy = gy2 + rr, gx = gx2 + cc;
-      float v = 0.f;
-      if (gc < C && (unsigned)gy < (unsigned)H && (unsigned)gx < (unsigned)W)
-        v = x2b[gc * HW + gy * W + gx];
-      s2[c * (R2 * XS) + rr * XS + cc] = v;
-    }
-    __syncthreads();
+    const bool more = c0 + CC < C;
+    if (more) fetch(c0 + CC);  // in flight during this stage's FMAs
     if (active) {
 #pragma unroll 2
       for (int c = 0; c < CC; ++c) {
@@ -137,6 +167,10 @@ __global__ __launch_bounds__(64 * NDY) void corr_fwd_kernel(const float* __restr
       }
     }
     __syncthreads();
+    if (more) {
+      stash();
+      __syncthreads();
+    }
   }
 
   if (!active) return;
@@ -163,14 +197,14 @@ __global__ __launch_bounds__(64 * NDY) void corr_fwd_kernel(const float* __restr
   }
 }
 
-template <int D, int PX, int SEGX, int NDY>
+template <int D, int PX, int SEGX, int NDY, int CC>
 hipError_t launch_fwd(const float* x1, const float* x2, float* out, int B, int C, int H, int W,
                       hipStream_t s) {
-  using F = FwdCfg<D, PX, SEGX, NDY, 8>;
+  using F = FwdCfg<D, PX, SEGX, NDY, CC>;
   const int tiles_x = (W + F::TW - 1) / F::TW;
   const int tiles_y = (H + F::TH - 1) / F::TH;
   dim3 grid(F::NDYG, tiles_x * tiles_y, B);
-  hipLaunchKernelGGL((corr_fwd_kernel<D, PX, SEGX, NDY, 8>), grid, dim3(F::NT), 0, s, x1, x2,
+  hipLaunchKernelGGL((corr_fwd_kernel<D, PX, SEGX, NDY, CC>), grid, dim3(F::NT), 0, s, x1, x2,
                      out, C, H, W, tiles_x);
   return hipGetLastError();
 }
@@ -183,10 +217,10 @@ hipError_t fwd_dispatch(const float* x1, const float* x2, float* out, int B, int
   // row: x1/x2 staged once); fall back to smaller tiles / split displacement
   // rows when that would leave most of the 256 CUs idle.
   const long big = (long)B * ((W + 63) / 64) * ((H + 7) / 8);
-  if (big >= 256) return launch_fwd<D, 8, 8, K>(x1, x2, out, B, C, H, W, s);
+  if (big >= 256) return launch_fwd<D, 8, 8, K, 4>(x1, x2, out, B, C, H, W, s);
   const long mid = (long)B * ((W + 31) / 32) * ((H + 7) / 8);
-  if (mid >= 256) return launch_fwd<D, 4, 8, K>(x1, x2, out, B, C, H, W, s);
-  return launch_fwd<D, 4, 8, 3>(x1, x2, out, B, C, H, W, s);
+  if (mid >= 256) return launch_fwd<D, 4, 8, K, 8>(x1, x2, out, B, C, H, W, s);
+  return launch_fwd<D, 4, 8, 3, 8>(x1, x2, out, B, C, H, W, s);
 }
 
 // --------------------------------------------------------------- backward --
@@ -234,17 +268,34 @@ __global__ __launch_bounds__(64 * NW) void corr_bwd_kernel(const float* __restri
   const float* xsb = xs + (size_t)b * C * HW;
   const float* gb = g + (size_t)b * K * K * HW;
 
-  // stage xs rows [y0-D, y0+TH+D) x cols [x0-D, x0+TW+D) for CC channels
-  for (int e = tid; e < CC * R * C2; e += NT) {
-    const int c = e / (R * C2);
-    const int rem = e - c * (R * C2);
-    const int rr = rem / C2;
-    const int cc = rem - rr * C2;
-    const int gc = c0 + c, gy = y0 - D + rr, gxx = x0 - D + cc;
-    float v = 0.f;
-    if (gc < C && (unsigned)gy < (unsigned)H && (unsigned)gxx < (unsigned)W)
-      v = xsb[gc * HW + gy * W + gxx];
-    sm[c * (R * XS) + rr * XS + cc] = v;
+  // stage xs rows [y0-D, y0+TH+D) x cols [x0-D, x0+TW+D) for CC channels:
+  // all loads in flight first (clamped unconditional loads), then LDS writes
+  {
+    constexpr int N = CC * R * C2, L = (N + NT - 1) / NT;
+    constexpr int CH = 16;  // loads in flight per batch (caps the staging registers)
+#pragma unroll 1
+    for (int k0 = 0; k0 < L; k0 += CH) {
+      float v[CH];
+#pragma unroll
+      for (int j = 0; j < CH; ++j) {
+        const int e = tid + (k0 + j) * NT;
+        const int c = e / (R * C2);
+        const int rem = e - c * (R * C2);
+        const int rr = rem / C2, cc = rem - (rem / C2) * C2;
+        const int gy = y0 - D + rr, gxx = x0 - D + cc;
+        const bool ok = e < N && c0 + c < C && (unsigned)gy < (unsigned)H && (unsigned)gxx < (unsigned)W;
+        const float t = xsb[ok ? (c0 + c) * HW + gy * W + gxx : 0];
+        v[j] = ok ? t : 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < CH; ++j) {
+        const int e = tid + (k0 + j) * NT;
+        const int c = e / (R * C2);
+        const int rem = e - c * (R * C2);
+        const int rr = rem / C2, cc = rem - (rem / C2) * C2;
+        if (e < N) sm[c * (R * XS) + rr * XS + cc] = v[j];
+      }
+    }
   }
   __syncthreads();
 
@@ -263,7 +314,11 @@ __global__ __launch_bounds__(64 * NW) void corr_bwd_kernel(const float* __restri
       for (int dx = 0; dx < K; ++dx) {
         const float* gp = gb + (dy * K + dx) * HW + y * W + xb;
 #pragma unroll
-        for (int i = 0; i < PX; ++i) gv[dx][i] = (rowok && xb + i < W) ? gp[i] : 0.f;
+        for (int i = 0; i < PX; ++i) {
+          const bool ok = rowok && xb + i < W;
+          const float t = gp[ok ? i : 0 - (y * W + xb)];  // clamped to the plane start
+          gv[dx][i] = ok ? t : 0.f;
+        }
       }
     } else {
       // g at the source pixels: g[b, dy*K+dx, y-(dy-D), xb+i-(dx-D)]
@@ -274,8 +329,11 @@ __global__ __launch_bounds__(64 * NW) void corr_bwd_kernel(const float* __restri
         const int xx0 = xb - dx + D;
         const float* gp = gb + (dy * K + dx) * HW + yy * W + xx0;
 #pragma unroll
-        for (int i = 0; i < PX; ++i)
-          gv[dx][i] = (rowok && (unsigned)(xx0 + i) < (unsigned)W) ? gp[i] : 0.f;
+        for (int i = 0; i < PX; ++i) {
+          const bool ok = rowok && (unsigned)(xx0 + i) < (unsigned)W;
+          const float t = gp[ok ? i : 0 - (yy * W + xx0)];  // clamped to the plane start
+          gv[dx][i] = ok ? t : 0.f;
+        }
       }
     }
     const int rs = G2 ? (2 * D - dy) : dy;

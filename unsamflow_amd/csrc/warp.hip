@@ -17,9 +17,9 @@
 // times (W-1)/2 (zero where the border clamp is active: ix<=0 or ix>=W-1),
 // then through norm_grid's autograd: du = (dgx/(W-1))*2.
 //
-// Layout: one lane per output pixel (consecutive lanes = consecutive x, so
-// flow/out/gout accesses are coalesced), channels looped inside the lane with
-// the 4 corner offsets and weights computed once per pixel. grad_x uses fp32
+// Layout: one lane per (output pixel, channel slice); consecutive lanes =
+// consecutive x, so flow/out/gout accesses are coalesced; the 4 corner offsets
+// and weights are computed once per lane and reused over its channels. grad_x uses fp32
 // global atomics (global_atomic_add_f32, no CAS loop); grad_flow is a
 // per-lane reduction over channels, written once (deterministic).
 #include "usf_common.h"
@@ -81,33 +81,40 @@ __device__ __forceinline__ Tap make_tap(float u, float v, int x, int y, int H, i
   return t;
 }
 
-template <bool BORDER>
+// Work split: a 256-thread workgroup covers PXB = 256/CS consecutive pixels x
+// CS channel slices (thread t: pixel t % PXB, channels t/PXB, t/PXB + CS, ...),
+// so consecutive lanes stay on consecutive pixels (coalesced flow/out/gout and
+// near-contiguous corner gathers / atomics) while small, channel-heavy pyramid
+// levels still spread over many workgroups instead of looping C channels per
+// lane.
+template <bool BORDER, int CS>
 __global__ __launch_bounds__(256) void warp_fwd_kernel(const float* __restrict__ x,
                                                        const float* __restrict__ flow,
                                                        long long fbs, float* __restrict__ out,
                                                        int B, int C, int H, int W) {
+  constexpr int PXB = 256 / CS;
   const int HW = H * W;
-  const int p = blockIdx.x * 256 + threadIdx.x;  // pixel within the sample
+  const int t = threadIdx.x;
+  const int slice = t / PXB;
+  const int p = blockIdx.x * PXB + (t - slice * PXB);
   const int b = blockIdx.y;
   if (p >= HW) return;
   const int y = p / W, xx = p - y * W;
   const float* fb = flow + b * fbs;
-  const Tap t = make_tap(fb[p], fb[HW + p], xx, y, H, W, BORDER);
-  const float wnw = t.s * t.e, wne = t.s * t.w, wsw = t.n * t.e, wse = t.n * t.w;
+  const Tap tp = make_tap(fb[p], fb[HW + p], xx, y, H, W, BORDER);
+  const float wnw = tp.s * tp.e, wne = tp.s * tp.w, wsw = tp.n * tp.e, wse = tp.n * tp.w;
   const float* xb = x + (size_t)b * C * HW;
   float* ob = out + (size_t)b * C * HW + p;
 #pragma unroll 4
-  for (int c = 0; c < C; ++c) {
+  for (int c = slice; c < C; c += CS) {
     const float* xc = xb + (size_t)c * HW;
-    const float vnw = t.m_nw ? xc[t.o_nw] : 0.f;
-    const float vne = t.m_ne ? xc[t.o_ne] : 0.f;
-    const float vsw = t.m_sw ? xc[t.o_sw] : 0.f;
-    const float vse = t.m_se ? xc[t.o_se] : 0.f;
-    ob[(size_t)c * HW] = vnw * wnw + vne * wne + vsw * wsw + vse * wse;
+    const float vnw = xc[tp.o_nw], vne = xc[tp.o_ne], vsw = xc[tp.o_sw], vse = xc[tp.o_se];
+    ob[(size_t)c * HW] = (tp.m_nw ? vnw : 0.f) * wnw + (tp.m_ne ? vne : 0.f) * wne +
+                         (tp.m_sw ? vsw : 0.f) * wsw + (tp.m_se ? vse : 0.f) * wse;
   }
 }
 
-template <bool BORDER, bool WANT_GX, bool WANT_GF>
+template <bool BORDER, bool WANT_GX, bool WANT_GF, int CS>
 __global__ __launch_bounds__(256) void warp_bwd_kernel(const float* __restrict__ x,
                                                        const float* __restrict__ flow,
                                                        long long fbs,
@@ -115,73 +122,132 @@ __global__ __launch_bounds__(256) void warp_bwd_kernel(const float* __restrict__
                                                        float* __restrict__ gx,
                                                        float* __restrict__ gflow, int B, int C,
                                                        int H, int W) {
+  constexpr int PXB = 256 / CS;
+  __shared__ float red[2][256];
   const int HW = H * W;
-  const int p = blockIdx.x * 256 + threadIdx.x;
+  const int t = threadIdx.x;
+  const int slice = t / PXB;
+  const int pl = t - slice * PXB;
+  const int p = blockIdx.x * PXB + pl;
   const int b = blockIdx.y;
-  if (p >= HW) return;
-  const int y = p / W, xx = p - y * W;
-  const float* fb = flow + b * fbs;
-  const Tap t = make_tap(fb[p], fb[HW + p], xx, y, H, W, BORDER);
-  const float wnw = t.s * t.e, wne = t.s * t.w, wsw = t.n * t.e, wse = t.n * t.w;
-  const float* xb = x + (size_t)b * C * HW;
-  const float* gb = gout + (size_t)b * C * HW + p;
-  float* gxb = WANT_GX ? gx + (size_t)b * C * HW : nullptr;
+  const bool valid = p < HW;
   float dix = 0.f, diy = 0.f;
+  Tap tp{};
+  if (valid) {
+    const int y = p / W, xx = p - y * W;
+    const float* fb = flow + b * fbs;
+    tp = make_tap(fb[p], fb[HW + p], xx, y, H, W, BORDER);
+    const float wnw = tp.s * tp.e, wne = tp.s * tp.w, wsw = tp.n * tp.e, wse = tp.n * tp.w;
+    const float* xb = x + (size_t)b * C * HW;
+    const float* gb = gout + (size_t)b * C * HW + p;
+    float* gxb = WANT_GX ? gx + (size_t)b * C * HW : nullptr;
 #pragma unroll 4
-  for (int c = 0; c < C; ++c) {
-    const float go = gb[(size_t)c * HW];
-    if (WANT_GX) {
-      float* gc = gxb + (size_t)c * HW;
-      if (t.m_nw) atomicAdd(gc + t.o_nw, go * wnw);
-      if (t.m_ne) atomicAdd(gc + t.o_ne, go * wne);
-      if (t.m_sw) atomicAdd(gc + t.o_sw, go * wsw);
-      if (t.m_se) atomicAdd(gc + t.o_se, go * wse);
-    }
-    if (WANT_GF) {
-      const float* xc = xb + (size_t)c * HW;
-      const float vnw = t.m_nw ? xc[t.o_nw] : 0.f;
-      const float vne = t.m_ne ? xc[t.o_ne] : 0.f;
-      const float vsw = t.m_sw ? xc[t.o_sw] : 0.f;
-      const float vse = t.m_se ? xc[t.o_se] : 0.f;
-      dix += ((vne - vnw) * t.s + (vse - vsw) * t.n) * go;
-      diy += ((vsw - vnw) * t.e + (vse - vne) * t.w) * go;
+    for (int c = slice; c < C; c += CS) {
+      const float go = gb[(size_t)c * HW];
+      if (WANT_GX) {
+        float* gc = gxb + (size_t)c * HW;
+        if (tp.m_nw) atomicAdd(gc + tp.o_nw, go * wnw);
+        if (tp.m_ne) atomicAdd(gc + tp.o_ne, go * wne);
+        if (tp.m_sw) atomicAdd(gc + tp.o_sw, go * wsw);
+        if (tp.m_se) atomicAdd(gc + tp.o_se, go * wse);
+      }
+      if (WANT_GF) {
+        const float* xc = xb + (size_t)c * HW;
+        const float vnw = tp.m_nw ? xc[tp.o_nw] : 0.f;
+        const float vne = tp.m_ne ? xc[tp.o_ne] : 0.f;
+        const float vsw = tp.m_sw ? xc[tp.o_sw] : 0.f;
+        const float vse = tp.m_se ? xc[tp.o_se] : 0.f;
+        dix += ((vne - vnw) * tp.s + (vse - vsw) * tp.n) * go;
+        diy += ((vsw - vnw) * tp.e + (vse - vne) * tp.w) * go;
+      }
     }
   }
   if (WANT_GF) {
+    if (CS > 1) {  // combine the channel slices in a fixed order (deterministic)
+      red[0][t] = dix;
+      red[1][t] = diy;
+      __syncthreads();
+      if (slice != 0) return;
+#pragma unroll
+      for (int k = 1; k < CS; ++k) {
+        dix += red[0][pl + k * PXB];
+        diy += red[1][pl + k * PXB];
+      }
+    }
+    if (!valid) return;
     // grid grad, then norm_grid's autograd (DivBackward by (W-1), MulBackward by 2)
-    const float ggx = dix * t.mx, ggy = diy * t.my;
+    const float ggx = dix * tp.mx, ggy = diy * tp.my;
     float* gf = gflow + (size_t)b * 2 * HW + p;
     gf[0] = (ggx / (float)(W - 1)) * 2.0f;
     gf[HW] = (ggy / (float)(H - 1)) * 2.0f;
   }
 }
 
+// Channel slices per workgroup: the smallest CS in {1,4,16,64} giving >= 1024
+// workgroups (8 XCDs x 32 CUs x 4), capped by C.
+inline int pick_cs(int B, int C, int HW) {
+  const int opts[4] = {1, 4, 16, 64};
+  for (int i = 0; i < 4; ++i) {
+    const int cs = opts[i];
+    const long blocks = (long)B * ((HW + 256 / cs - 1) / (256 / cs));
+    if (blocks >= 1024 || cs >= C || i == 3) return cs;
+  }
+  return 64;
+}
+
+template <bool BORDER, int CS>
+void fwd_launch_cs(const float* x, const float* flow, long long fbs, float* out, int B, int C,
+                   int H, int W, hipStream_t s) {
+  const dim3 grid((unsigned)((H * W + 256 / CS - 1) / (256 / CS)), (unsigned)B), block(256);
+  hipLaunchKernelGGL((warp_fwd_kernel<BORDER, CS>), grid, block, 0, s, x, flow, fbs, out, B, C, H,
+                     W);
+}
+
 template <bool BORDER>
-hipError_t bwd_launch_pad(const float* x, const float* flow, long long fbs, const float* gout,
-                          float* gx, float* gflow, int B, int C, int H, int W, hipStream_t s) {
-  const dim3 grid((unsigned)((H * W + 255) / 256), (unsigned)B), block(256);
+void fwd_launch_pad(const float* x, const float* flow, long long fbs, float* out, int B, int C,
+                    int H, int W, hipStream_t s) {
+  switch (pick_cs(B, C, H * W)) {
+    case 1: fwd_launch_cs<BORDER, 1>(x, flow, fbs, out, B, C, H, W, s); break;
+    case 4: fwd_launch_cs<BORDER, 4>(x, flow, fbs, out, B, C, H, W, s); break;
+    case 16: fwd_launch_cs<BORDER, 16>(x, flow, fbs, out, B, C, H, W, s); break;
+    default: fwd_launch_cs<BORDER, 64>(x, flow, fbs, out, B, C, H, W, s); break;
+  }
+}
+
+template <bool BORDER, int CS>
+void bwd_launch_cs(const float* x, const float* flow, long long fbs, const float* gout, float* gx,
+                   float* gflow, int B, int C, int H, int W, hipStream_t s) {
+  const dim3 grid((unsigned)((H * W + 256 / CS - 1) / (256 / CS)), (unsigned)B), block(256);
   if (gx && gflow)
-    hipLaunchKernelGGL((warp_bwd_kernel<BORDER, true, true>), grid, block, 0, s, x, flow, fbs,
+    hipLaunchKernelGGL((warp_bwd_kernel<BORDER, true, true, CS>), grid, block, 0, s, x, flow, fbs,
                        gout, gx, gflow, B, C, H, W);
   else if (gx)
-    hipLaunchKernelGGL((warp_bwd_kernel<BORDER, true, false>), grid, block, 0, s, x, flow, fbs,
-                       gout, gx, gflow, B, C, H, W);
-  else if (gflow)
-    hipLaunchKernelGGL((warp_bwd_kernel<BORDER, false, true>), grid, block, 0, s, x, flow, fbs,
-                       gout, gx, gflow, B, C, H, W);
-  return hipGetLastError();
+    hipLaunchKernelGGL((warp_bwd_kernel<BORDER, true, false, CS>), grid, block, 0, s, x, flow,
+                       fbs, gout, gx, gflow, B, C, H, W);
+  else
+    hipLaunchKernelGGL((warp_bwd_kernel<BORDER, false, true, CS>), grid, block, 0, s, x, flow,
+                       fbs, gout, gx, gflow, B, C, H, W);
+}
+
+template <bool BORDER>
+void bwd_launch_pad(const float* x, const float* flow, long long fbs, const float* gout,
+                    float* gx, float* gflow, int B, int C, int H, int W, hipStream_t s) {
+  switch (pick_cs(B, C, H * W)) {
+    case 1: bwd_launch_cs<BORDER, 1>(x, flow, fbs, gout, gx, gflow, B, C, H, W, s); break;
+    case 4: bwd_launch_cs<BORDER, 4>(x, flow, fbs, gout, gx, gflow, B, C, H, W, s); break;
+    case 16: bwd_launch_cs<BORDER, 16>(x, flow, fbs, gout, gx, gflow, B, C, H, W, s); break;
+    default: bwd_launch_cs<BORDER, 64>(x, flow, fbs, gout, gx, gflow, B, C, H, W, s); break;
+  }
 }
 
 }  // namespace
 
 hipError_t warp_fwd_launch(const float* x, const float* flow, long long fbs, float* out, int B,
                            int C, int H, int W, int pad_mode, hipStream_t s) {
-  const dim3 grid((unsigned)((H * W + 255) / 256), (unsigned)B), block(256);
   if (pad_mode == 1)
-    hipLaunchKernelGGL((warp_fwd_kernel<true>), grid, block, 0, s, x, flow, fbs, out, B, C, H, W);
+    fwd_launch_pad<true>(x, flow, fbs, out, B, C, H, W, s);
   else
-    hipLaunchKernelGGL((warp_fwd_kernel<false>), grid, block, 0, s, x, flow, fbs, out, B, C, H,
-                       W);
+    fwd_launch_pad<false>(x, flow, fbs, out, B, C, H, W, s);
   return hipGetLastError();
 }
 
@@ -189,8 +255,11 @@ hipError_t warp_bwd_launch(const float* x, const float* flow, long long fbs, con
                            float* gx, float* gflow, int B, int C, int H, int W, int pad_mode,
                            hipStream_t s) {
   if (!gx && !gflow) return hipSuccess;
-  if (pad_mode == 1) return bwd_launch_pad<true>(x, flow, fbs, gout, gx, gflow, B, C, H, W, s);
-  return bwd_launch_pad<false>(x, flow, fbs, gout, gx, gflow, B, C, H, W, s);
+  if (pad_mode == 1)
+    bwd_launch_pad<true>(x, flow, fbs, gout, gx, gflow, B, C, H, W, s);
+  else
+    bwd_launch_pad<false>(x, flow, fbs, gout, gx, gflow, B, C, H, W, s);
+  return hipGetLastError();
 }
 
 }  // namespace usf
