@@ -285,3 +285,26 @@ def test_warp_integer_shift_matches_roll(hip_device):
     rows = torch.clamp(torch.arange(20, device=hip_device) - 2, 0, 19)
     ref = x[:, :, rows][:, :, :, cols]
     torch.testing.assert_close(out, ref, atol=5e-6, rtol=0)
+
+
+def test_correlation_cuda_shim_reference_call_pattern(hip_device):
+    """The reference's correlation.py:9-72 call sequence against the
+    correlation_cuda-compatible shim: empty tensors from .new(), resized and
+    filled by the callee, return value 1."""
+    from unsamflow_amd import correlation_cuda
+
+    shape = (2, 16, 9, 30)
+    x1 = hashrng.normal(shape, 41)
+    x2 = hashrng.normal(shape, 42)
+    g = hashrng.normal((2, 81, 9, 30), 43)
+    t1, t2 = _dev(x1, hip_device), _dev(x2, hip_device)
+    rbot1, rbot2, output = t1.new(), t2.new(), t1.new()
+    assert correlation_cuda.forward(t1, t2, rbot1, rbot2, output, 4, 1, 4, 1, 1, 1) == 1
+    np.testing.assert_allclose(_np(output), corr_forward_np(x1, x2, 4), atol=CORR_ATOL, rtol=CORR_RTOL)
+    gi1, gi2 = t1.new(), t2.new()
+    assert correlation_cuda.backward(t1, t2, t1.new(), t2.new(), _dev(g, hip_device), gi1, gi2, 4, 1, 4, 1, 1, 1) == 1
+    r1, r2 = corr_backward_np(x1, x2, g, 4)
+    np.testing.assert_allclose(_np(gi1), r1, atol=CORR_ATOL, rtol=CORR_RTOL)
+    np.testing.assert_allclose(_np(gi2), r2, atol=CORR_ATOL, rtol=CORR_RTOL)
+    with pytest.raises(NotImplementedError):
+        correlation_cuda.forward(t1, t2, rbot1, rbot2, output, 3, 3, 20, 1, 2, 1)

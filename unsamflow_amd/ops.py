@@ -31,14 +31,22 @@ def _require_device_f32(name: str, t: torch.Tensor) -> None:
         raise TypeError(f"unsamflow_amd: {name} must be float32, got {t.dtype}")
 
 
+def _check_out(name: str, t: torch.Tensor, shape, device) -> None:
+    if tuple(t.shape) != tuple(shape) or t.dtype != torch.float32 or t.device != device or not t.is_contiguous():
+        raise ValueError(f"{name} must be a contiguous float32 {tuple(shape)} tensor on {device}")
+
+
 def _nchw(name: str, t: torch.Tensor) -> tuple[int, int, int, int]:
     if t.dim() != 4:
         raise ValueError(f"{name} must be 4-D NCHW, got shape {tuple(t.shape)}")
     return tuple(t.shape)  # type: ignore[return-value]
 
 
-def corr_forward(x1: torch.Tensor, x2: torch.Tensor, max_displacement: int) -> torch.Tensor:
-    """Cost volume [B,(2d+1)^2,H,W] of x1 against x2 (correlation_native.py:13-23)."""
+def corr_forward(x1: torch.Tensor, x2: torch.Tensor, max_displacement: int,
+                 out: torch.Tensor | None = None) -> torch.Tensor:
+    """Cost volume [B,(2d+1)^2,H,W] of x1 against x2 (correlation_native.py:13-23).
+
+    ``out``: optional preallocated contiguous fp32 output of the right shape."""
     _require_device_f32("input1", x1)
     _require_device_f32("input2", x2)
     B, C, H, W = _nchw("input1", x1)
@@ -49,7 +57,10 @@ def corr_forward(x1: torch.Tensor, x2: torch.Tensor, max_displacement: int) -> t
     d = int(max_displacement)
     K = 2 * d + 1
     x1c, x2c = x1.contiguous(), x2.contiguous()
-    out = torch.empty((B, K * K, H, W), device=x1.device, dtype=torch.float32)
+    if out is None:
+        out = torch.empty((B, K * K, H, W), device=x1.device, dtype=torch.float32)
+    else:
+        _check_out("output", out, (B, K * K, H, W), x1.device)
     lib = _lib.load()
     with torch.cuda.device(x1.device), _kt.timed(
         "corr_fwd", (B, C, H, W), x1.device, _kt.corr_bytes(B, C, H, W, K * K), _kt.corr_flops(B, C, H, W, K * K)
@@ -68,8 +79,12 @@ def corr_backward(
     max_displacement: int,
     need_x1: bool = True,
     need_x2: bool = True,
+    gx1_out: torch.Tensor | None = None,
+    gx2_out: torch.Tensor | None = None,
 ) -> tuple[torch.Tensor | None, torch.Tensor | None]:
-    """(grad_input1, grad_input2) of :func:`corr_forward`; deterministic."""
+    """(grad_input1, grad_input2) of :func:`corr_forward`; deterministic.
+
+    ``gx1_out`` / ``gx2_out``: optional preallocated contiguous outputs."""
     _require_device_f32("input1", x1)
     _require_device_f32("input2", x2)
     _require_device_f32("grad_output", grad_out)
@@ -81,8 +96,13 @@ def corr_backward(
     if not (need_x1 or need_x2):
         return None, None
     x1c, x2c, gc = x1.contiguous(), x2.contiguous(), grad_out.contiguous()
-    g1 = torch.empty_like(x1c) if need_x1 else None
-    g2 = torch.empty_like(x2c) if need_x2 else None
+    g1 = g2 = None
+    if need_x1:
+        g1 = torch.empty_like(x1c) if gx1_out is None else gx1_out
+        _check_out("grad_input1", g1, (B, C, H, W), x1.device)
+    if need_x2:
+        g2 = torch.empty_like(x2c) if gx2_out is None else gx2_out
+        _check_out("grad_input2", g2, (B, C, H, W), x1.device)
     lib = _lib.load()
     with torch.cuda.device(x1.device), _kt.timed(
         "corr_bwd", (B, C, H, W, need_x1, need_x2), x1.device,
