@@ -102,8 +102,10 @@ def timed(op: str, key, device, nbytes: int, flops: int = 0):
 def site_launcher(op: str, key, device, seed: int = 0):
     """A closure launching one kernel of call site (op, key) on synthetic inputs.
 
-    Inputs: N(0,1) features / gradients; warp flows U[-2,2) px (the magnitude
-    of the decoder's and loss's flows early in training) and U[0,1) images.
+    Inputs: N(0,1) features / gradients, U[0,1) images, and a smooth warp flow
+    of +-2 px amplitude (two low-frequency sinusoids per component: the
+    magnitude and smoothness of PWCLite's flows early in training). Per-pixel
+    random flows would scatter the grad_x atomics and misstate the kernel.
     """
     from . import ops
 
@@ -119,7 +121,10 @@ def site_launcher(op: str, key, device, seed: int = 0):
         return lambda: ops.corr_backward(x1, x2, go, 4, need1, need2)
     B, C, H, W, pad = key[:5]
     x = torch.rand(B, C, H, W, device=device, generator=g)
-    flow = (torch.rand(B, 2, H, W, device=device, generator=g) - 0.5) * 4
+    yy = torch.linspace(0, 6.2832, H, device=device).view(1, 1, H, 1)
+    xx = torch.linspace(0, 6.2832, W, device=device).view(1, 1, 1, W)
+    ph = torch.rand(B, 2, 1, 1, device=device, generator=g) * 6.2832
+    flow = (torch.sin(2 * xx + ph) + torch.cos(3 * yy - ph)).contiguous()  # [B,2,H,W], |f| <= 2
     if op == "warp_fwd":
         return lambda: ops.warp_forward(x, flow, pad)
     need_x, need_flow = key[5], key[6]
