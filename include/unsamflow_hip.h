@@ -26,7 +26,7 @@
  *     (losses/flow_loss.py:130-131) need no copy.
  *   - The caller allocates every output; the library never allocates,
  *     never keeps a pointer after return and has no global state except a
- *     thread-local error string. Calls are reentrant (the backward runs on the
+ *     thread-local error string and the usf_set_variant tuning override. Calls are reentrant (the backward runs on the
  *     autograd engine's device thread).
  *   - Calls are asynchronous on `stream` (a hipStream_t; NULL = legacy
  *     default stream).
@@ -91,6 +91,15 @@ int usf_warp_fwd_f32(const float* x, const float* flow, long long flow_bstride,
 int usf_warp_bwd_f32(const float* x, const float* flow, long long flow_bstride,
                      const float* gout, float* gx, float* gflow,
                      int B, int C, int H, int W, int pad_mode, void* stream);
+
+/* Tuning hook (benchmarking only; not needed for correct use).
+ * Forces kernel variant `index` of `op` for d=4 launches in this process:
+ * op 0 = correlation forward tile config, op 1 = correlation backward tile
+ * config; index -1 restores the built-in shape heuristic. Returns the number of
+ * variants of `op` (so index range is [0, n)), or USF_EINVAL for an unknown op
+ * or out-of-range index. Process-wide; set it before launching, not
+ * concurrently with launches. */
+int usf_set_variant(int op, int index);
 
 #ifdef __cplusplus
 }

@@ -31,7 +31,7 @@ def test_header_declares_the_abi():
     syms = declared_symbols()
     assert syms == sorted(
         ["usf_abi_version", "usf_last_error_string", "usf_corr_fwd_f32", "usf_corr_bwd_f32",
-         "usf_warp_fwd_f32", "usf_warp_bwd_f32"]
+         "usf_warp_fwd_f32", "usf_warp_bwd_f32", "usf_set_variant"]
     )
 
 
@@ -89,6 +89,16 @@ def test_error_string_cleared_on_next_call(lib):
     # a warp bwd with neither output requested is a valid no-op (no launch)
     assert lib.usf_warp_bwd_f32(1, 1, 32, 1, None, None, 1, 3, 4, 4, 1, None) == 0
     assert lib.usf_last_error_string() == b""
+
+
+def test_variant_override_bounds(lib):
+    n_fwd = lib.usf_set_variant(0, -1)
+    n_bwd = lib.usf_set_variant(1, -1)
+    assert n_fwd > 1 and n_bwd > 1
+    assert lib.usf_set_variant(0, n_fwd) == -1 and b"bad op" in lib.usf_last_error_string()
+    assert lib.usf_set_variant(2, 0) == -1
+    assert lib.usf_set_variant(1, n_bwd - 1) == n_bwd
+    assert lib.usf_set_variant(1, -1) == n_bwd
 
 
 def test_ctypes_signatures_match_header():

@@ -308,3 +308,31 @@ def test_correlation_cuda_shim_reference_call_pattern(hip_device):
     np.testing.assert_allclose(_np(gi2), r2, atol=CORR_ATOL, rtol=CORR_RTOL)
     with pytest.raises(NotImplementedError):
         correlation_cuda.forward(t1, t2, rbot1, rbot2, output, 3, 3, 20, 1, 2, 1)
+
+
+@pytest.mark.parametrize("shape", [(2, 40, 13, 37), (1, 192, 4, 13), (2, 32, 64, 70)])
+def test_corr_every_tile_variant_vs_oracle(hip_device, shape):
+    """Every d=4 tile variant reachable through usf_set_variant computes the same result."""
+    from unsamflow_amd import _lib, ops
+
+    lib = _lib.load()
+    B, C, H, W = shape
+    x1 = hashrng.normal(shape, 61)
+    x2 = hashrng.normal(shape, 62)
+    g = hashrng.normal((B, 81, H, W), 63)
+    t1, t2, tg = _dev(x1, hip_device), _dev(x2, hip_device), _dev(g, hip_device)
+    ref = corr_forward_np(x1, x2, 4)
+    r1, r2 = corr_backward_np(x1, x2, g, 4)
+    try:
+        for v in range(lib.usf_set_variant(0, -1)):
+            lib.usf_set_variant(0, v)
+            np.testing.assert_allclose(_np(ops.corr_forward(t1, t2, 4)), ref, atol=CORR_ATOL, rtol=CORR_RTOL,
+                                       err_msg=f"fwd variant {v}")
+        for v in range(lib.usf_set_variant(1, -1)):
+            lib.usf_set_variant(1, v)
+            gx1, gx2 = ops.corr_backward(t1, t2, tg, 4)
+            np.testing.assert_allclose(_np(gx1), r1, atol=CORR_ATOL, rtol=CORR_RTOL, err_msg=f"bwd variant {v}")
+            np.testing.assert_allclose(_np(gx2), r2, atol=CORR_ATOL, rtol=CORR_RTOL, err_msg=f"bwd variant {v}")
+    finally:
+        lib.usf_set_variant(0, -1)
+        lib.usf_set_variant(1, -1)

@@ -44,6 +44,7 @@ _SIGNATURES = {
         + [ctypes.c_void_p],
         ctypes.c_int,
     ),
+    "usf_set_variant": ([ctypes.c_int, ctypes.c_int], ctypes.c_int),
 }
 EXPORTED_SYMBOLS = tuple(_SIGNATURES)
 

@@ -209,10 +209,35 @@ hipError_t launch_fwd(const float* x1, const float* x2, float* out, int B, int C
   return hipGetLastError();
 }
 
+// Tuning hook: usf_set_variant(op, i) forces candidate i for d=4
+// (tools/kbench.py sweeps them on the GPU); -1 = the shape heuristic below.
+
+hipError_t fwd_candidate_d4(int i, const float* x1, const float* x2, float* out, int B, int C,
+                            int H, int W, hipStream_t s) {
+  switch (i) {
+    case 0: return launch_fwd<4, 8, 8, 9, 4>(x1, x2, out, B, C, H, W, s);
+    case 1: return launch_fwd<4, 4, 8, 9, 8>(x1, x2, out, B, C, H, W, s);
+    case 2: return launch_fwd<4, 4, 8, 3, 8>(x1, x2, out, B, C, H, W, s);
+    case 3: return launch_fwd<4, 8, 8, 3, 4>(x1, x2, out, B, C, H, W, s);
+    case 4: return launch_fwd<4, 4, 16, 3, 8>(x1, x2, out, B, C, H, W, s);
+    case 5: return launch_fwd<4, 4, 16, 9, 8>(x1, x2, out, B, C, H, W, s);
+    case 6: return launch_fwd<4, 8, 8, 1, 8>(x1, x2, out, B, C, H, W, s);
+    case 7: return launch_fwd<4, 4, 8, 1, 8>(x1, x2, out, B, C, H, W, s);
+    case 8: return launch_fwd<4, 4, 4, 3, 8>(x1, x2, out, B, C, H, W, s);
+    case 9: return launch_fwd<4, 4, 8, 3, 16>(x1, x2, out, B, C, H, W, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+constexpr int kFwdCandidates = 10;
+
 template <int D>
 hipError_t fwd_dispatch(const float* x1, const float* x2, float* out, int B, int C, int H,
                         int W, hipStream_t s) {
   constexpr int K = 2 * D + 1;
+  if (D == 4) {
+    const int forced = variant_override(0);
+    if (forced >= 0) return fwd_candidate_d4(forced, x1, x2, out, B, C, H, W, s);
+  }
   // Prefer the big tile (8 px/lane, one workgroup covers every displacement
   // row: x1/x2 staged once); fall back to smaller tiles / split displacement
   // rows when that would leave most of the 256 CUs idle.
@@ -380,10 +405,9 @@ __global__ __launch_bounds__(64 * NW) void corr_bwd_kernel(const float* __restri
   }
 }
 
-template <int D, bool G2>
+template <int D, bool G2, int PX = 4, int SEGX = 8, int NW = 3, int CC = 16>
 hipError_t launch_bwd(const float* xs, const float* g, float* gx, int B, int C, int H, int W,
                       hipStream_t s) {
-  constexpr int PX = 4, SEGX = 8, NW = 3, CC = 16;
   using F = BwdCfg<D, PX, SEGX, NW, CC>;
   const int tiles_x = (W + F::TW - 1) / F::TW;
   const int tiles_y = (H + F::TH - 1) / F::TH;
@@ -393,16 +417,44 @@ hipError_t launch_bwd(const float* xs, const float* g, float* gx, int B, int C, 
   return hipGetLastError();
 }
 
+template <bool G2>
+hipError_t bwd_candidate_d4(int i, const float* xs, const float* g, float* gx, int B, int C, int H,
+                            int W, hipStream_t s) {
+  switch (i) {
+    case 0: return launch_bwd<4, G2, 4, 8, 3, 16>(xs, g, gx, B, C, H, W, s);
+    case 1: return launch_bwd<4, G2, 4, 8, 3, 8>(xs, g, gx, B, C, H, W, s);
+    case 2: return launch_bwd<4, G2, 4, 16, 3, 16>(xs, g, gx, B, C, H, W, s);
+    case 3: return launch_bwd<4, G2, 4, 4, 3, 16>(xs, g, gx, B, C, H, W, s);
+    case 4: return launch_bwd<4, G2, 4, 8, 9, 8>(xs, g, gx, B, C, H, W, s);
+    case 5: return launch_bwd<4, G2, 4, 8, 1, 16>(xs, g, gx, B, C, H, W, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+constexpr int kBwdCandidates = 6;
+
 template <int D>
 hipError_t bwd_dispatch(const float* x1, const float* x2, const float* g, float* gx1, float* gx2,
                         int B, int C, int H, int W, hipStream_t s) {
   hipError_t e = hipSuccess;
+  if (D == 4) {
+    const int forced = variant_override(1);
+    if (forced >= 0) {
+      if (gx1) e = bwd_candidate_d4<false>(forced, x2, g, gx1, B, C, H, W, s);
+      if (e == hipSuccess && gx2) e = bwd_candidate_d4<true>(forced, x1, g, gx2, B, C, H, W, s);
+      return e;
+    }
+  }
   if (gx1) e = launch_bwd<D, false>(x2, g, gx1, B, C, H, W, s);
   if (e == hipSuccess && gx2) e = launch_bwd<D, true>(x1, g, gx2, B, C, H, W, s);
   return e;
 }
 
 }  // namespace
+
+static int g_variant[2] = {-1, -1};
+int variant_override(int op) { return __atomic_load_n(&g_variant[op], __ATOMIC_RELAXED); }
+int variant_count(int op) { return op == 0 ? kFwdCandidates : kBwdCandidates; }
+void set_variant_override(int op, int index) { __atomic_store_n(&g_variant[op], index, __ATOMIC_RELAXED); }
 
 hipError_t corr_fwd_launch(const float* x1, const float* x2, float* out, int B, int C, int H,
                            int W, int d, hipStream_t s) {

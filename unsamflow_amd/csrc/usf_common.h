@@ -13,6 +13,11 @@ void clear_error();
 // Round n up to a multiple of m (compile-time helper).
 __host__ __device__ constexpr int round_up(int n, int m) { return ((n + m - 1) / m) * m; }
 
+// Tuning override of usf_set_variant (op 0: corr fwd, op 1: corr bwd; -1 = heuristic).
+int variant_override(int op);
+int variant_count(int op);
+void set_variant_override(int op, int index);
+
 // Launchers implemented in corr.hip / warp.hip. They assume validated
 // arguments (capi.cpp checks shapes, d and pointers) and return the
 // hipError_t of the launch.
