@@ -11,69 +11,97 @@
 // kernel_size=1, stride1=stride2=1, pad=d, which is what pwclite.py:208-215 uses.
 //
 // Design (MI355X-first, not a translation of the CUDA kernels):
+//  * Staging is LDS-DMA (buffer_load_dword ... lds): a stage of CC channels is
+//    copied HBM->LDS by one wave-instruction per 64 consecutive elements of a
+//    channel's tile image, with no VGPR round trip and no per-element index
+//    math. Each chunk gets a buffer descriptor covering exactly one channel
+//    plane, so the zero padding outside the image (and the channel tail) is
+//    the hardware's out-of-range zero fill: off-image lanes carry an offset
+//    past num_records, channels >= C carry num_records = 0. The per-lane
+//    offsets are stage-invariant and computed once. Two LDS images: the DMA
+//    of stage s+1 is in flight while stage s is computed.
 //  * Forward: one workgroup = one output tile (TH rows x TW cols) x NDY
-//    displacement rows. Wave w owns displacement row dyb+w; lane l owns PX
-//    consecutive output pixels (row l/SEGX, segment l%SEGX). A channel stage of
-//    CC channels of the x1 tile and the (TH+NDY-1) x (TW+2d) x2 halo is staged
-//    in LDS (coalesced dword loads, zero fill = the zero padding), then each
-//    lane keeps K*PX accumulators in VGPRs and reads one x1 segment and one
-//    x2 window (PX+2d floats) per channel with ds_read_b128: K*PX FMAs per
-//    (2*PX+2d) LDS floats. No cross-lane reduction (the channel sum is a
-//    per-lane FMA chain), so no shared prod_sum/serial reduction as in the
-//    reference (.cu:84-109).
-//  * Backward: deterministic gather form, no atomics. gx1 and gx2 are the
-//    same kernel (G2 template flag): the output channel is independent, so a
-//    workgroup owns one tile x CC channels; wave w owns displacement rows
-//    w, w+NW, ...; per displacement row the lane loads its K*PX slice of g
-//    (coalesced along x) once and streams CC channels of the staged x halo
-//    from LDS. The NW per-wave partial sums are combined through LDS (which
-//    aliases the staging buffer) and written once, coalesced.
+//    displacement rows; wave w owns displacement row dyb+w, lane l owns PX
+//    consecutive pixels (row l/SEGX, segment l%SEGX) and keeps K*PX
+//    accumulators in VGPRs; per channel it reads an x1 segment and a PX+2d
+//    x2 window with ds_read_b128 (K*PX FMAs per 2*PX+2d LDS floats). The
+//    channel sum is a per-lane FMA chain: no cross-lane reduction.
+//  * Backward: deterministic gather form, no atomics. gx1 and gx2 are the same
+//    kernel (G2 flag, mirrored indices). A workgroup owns one tile x a channel
+//    group; wave w owns DYW displacement rows and keeps its DYW*K*PX slice of g
+//    in VGPRs for the whole channel loop (g read once per workgroup); per
+//    channel the DYW partial rows are summed in registers, the NW per-wave
+//    partials are added through LDS in a fixed order and written once.
 #include "usf_common.h"
 
 namespace usf {
 namespace {
 
+// gfx950 buffer descriptor word 3 for raw 32-bit loads (MI355X guide T8).
+constexpr int kRsrcFlags = 0x00020000;
+// a byte offset past any plane's num_records (planes are < 2 GiB, checked in capi.cpp)
+constexpr int kOffImage = 0x7FFFFFF0;
+
+using lds_void_t = __attribute__((address_space(3))) void;
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t plane_rsrc(const float* plane, bool valid,
+                                                           int plane_bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(plane), (short)0,
+                                           valid ? plane_bytes : 0, kRsrcFlags);
+}
+
+// One wave-instruction: 64 consecutive floats of LDS at `dst` (wave-uniform)
+// from per-lane byte offsets `voff` of the plane described by `rsrc`.
+__device__ __forceinline__ void dma64(__amdgpu_buffer_rsrc_t rsrc, float* dst, int voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void_t*)dst, 4, voff, 0, 0, 0);
+}
+
+__device__ __forceinline__ void dma_wait_all() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+template <int N>
+__device__ __forceinline__ void lds_read(const float* p, float (&v)[N]) {
+  static_assert(N % 4 == 0, "b128 reads");
+#pragma unroll
+  for (int i = 0; i < N / 4; ++i) {
+    const float4 t = reinterpret_cast<const float4*>(p)[i];
+    v[4 * i] = t.x; v[4 * i + 1] = t.y; v[4 * i + 2] = t.z; v[4 * i + 3] = t.w;
+  }
+}
+
 // ---------------------------------------------------------------- forward --
 template <int D, int PX, int SEGX, int NDY, int CC>
 struct FwdCfg {
   static constexpr int K = 2 * D + 1;
-  static constexpr int TW = SEGX * PX;          // tile width (pixels)
-  static constexpr int TH = 64 / SEGX;          // tile height (rows)
-  static constexpr int NT = 64 * NDY;           // threads per workgroup
-  static constexpr int NDYG = (K + NDY - 1) / NDY;
-  static constexpr int R2 = TH + NDY - 1;       // staged x2 rows
-  static constexpr int C2 = TW + 2 * D;         // staged x2 cols
+  static constexpr int TW = SEGX * PX;              // tile width (pixels)
+  static constexpr int TH = 64 / SEGX;              // tile height (rows)
+  static constexpr int NT = 64 * NDY;               // threads per workgroup
+  static constexpr int NDYG = (K + NDY - 1) / NDY;  // workgroups per tile
+  static constexpr int R2 = TH + NDY - 1;           // staged x2 rows
+  static constexpr int C2 = round_up(TW + 2 * D, 4);  // staged x2 cols (row stride)
+  static constexpr int P1 = TH * TW;                // x1 plane image (floats)
+  static constexpr int P2 = round_up(R2 * C2, 64);  // x2 plane image
+  static constexpr int CH1 = P1 / 64, CH2 = P2 / 64;  // 64-float chunks per plane
+  static constexpr int J1 = (CH1 + NDY - 1) / NDY;  // chunks per wave per plane
+  static constexpr int J2 = (CH2 + NDY - 1) / NDY;
   static constexpr int WIN = round_up(PX + 2 * D, 4);
-  static constexpr int XS = round_up(C2, 4) + 4;  // LDS row stride (floats)
-  static constexpr int N1 = CC * TH * TW;         // staged x1 elements per stage
-  static constexpr int N2 = CC * R2 * C2;         // staged x2 elements per stage
-  static constexpr int L1 = (N1 + NT - 1) / NT;   // per-thread staging registers
-  static constexpr int L2 = (N2 + NT - 1) / NT;
-  static constexpr int S1N = N1;
-  static constexpr int S2N = CC * R2 * XS + WIN;  // + tail pad for window over-read
+  static constexpr int STAGE = CC * (P1 + P2);
+  static constexpr int LDSN = 2 * STAGE + WIN;      // two images + window over-read pad
   static_assert(PX % 4 == 0, "PX must be a multiple of 4 (ds_read_b128)");
-  static_assert(64 % SEGX == 0, "SEGX must divide 64");
+  static_assert(64 % SEGX == 0 && P1 % 64 == 0, "tile must be whole 64-float chunks");
 };
 
-// Staging: every global load of a stage is issued before the first LDS write
-// (unconditional loads from clamped addresses, zero selected afterwards —
-// a per-element "load or 0" branch would make hipcc wait for each load in
-// turn), and the next stage's loads are in flight while the current stage is
-// computed (register double-buffering, one LDS image).
 template <int D, int PX, int SEGX, int NDY, int CC>
 __global__ __launch_bounds__(64 * NDY) void corr_fwd_kernel(const float* __restrict__ x1,
                                                             const float* __restrict__ x2,
                                                             float* __restrict__ out, int C,
                                                             int H, int W, int tiles_x) {
   using F = FwdCfg<D, PX, SEGX, NDY, CC>;
-  constexpr int K = F::K, TW = F::TW, TH = F::TH, NT = F::NT, R2 = F::R2, C2 = F::C2;
-  constexpr int WIN = F::WIN, XS = F::XS, N1 = F::N1, N2 = F::N2, L1 = F::L1, L2 = F::L2;
-  __shared__ __attribute__((aligned(16))) float s1[F::S1N];
-  __shared__ __attribute__((aligned(16))) float s2[F::S2N];
+  constexpr int K = F::K, TW = F::TW, TH = F::TH, C2 = F::C2, P1 = F::P1, P2 = F::P2;
+  constexpr int WIN = F::WIN, STAGE = F::STAGE;
+  __shared__ __attribute__((aligned(16))) float sm[F::LDSN];
 
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = tid >> 6;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int dyb = blockIdx.x * NDY;
   const int tile = blockIdx.y;
   const int b = blockIdx.z;
@@ -87,46 +115,35 @@ __global__ __launch_bounds__(64 * NDY) void corr_fwd_kernel(const float* __restr
   const int HW = H * W;
   const float* x1b = x1 + (size_t)b * C * HW;
   const float* x2b = x2 + (size_t)b * C * HW;
-  const int gy2 = y0 + dyb - D;  // image row of staged x2 row 0
-  const int gx2 = x0 - D;        // image col of staged x2 col 0
 
-  float r1[L1], r2[L2];
-  auto fetch = [&](int c0) {
+  // stage-invariant per-lane byte offsets of this wave's chunks
+  int vo1[F::J1], vo2[F::J2];
 #pragma unroll
-    for (int k = 0; k < L1; ++k) {
-      const int e = tid + k * NT;
-      const int c = e / (TH * TW);
-      const int rem = e - c * (TH * TW);
-      const int rr = rem / TW, cc = rem - (rem / TW) * TW;
-      const bool ok = e < N1 && c0 + c < C && y0 + rr < H && x0 + cc < W;
-      const float v = x1b[ok ? (c0 + c) * HW + (y0 + rr) * W + x0 + cc : 0];
-      r1[k] = ok ? v : 0.f;
-    }
+  for (int t = 0; t < F::J1; ++t) {
+    const int e = (wave + t * NDY) * 64 + lane;
+    const int gy = y0 + e / TW, gx = x0 + e % TW;
+    vo1[t] = (gy < H && gx < W) ? (gy * W + gx) * 4 : kOffImage;
+  }
 #pragma unroll
-    for (int k = 0; k < L2; ++k) {
-      const int e = tid + k * NT;
-      const int c = e / (R2 * C2);
-      const int rem = e - c * (R2 * C2);
-      const int rr = rem / C2, cc = rem - (rem / C2) * C2;
-      const int gy = gy2 + rr, gx = gx2 + cc;
-      const bool ok = e < N2 && c0 + c < C && (unsigned)gy < (unsigned)H && (unsigned)gx < (unsigned)W;
-      const float v = x2b[ok ? (c0 + c) * HW + gy * W + gx : 0];
-      r2[k] = ok ? v : 0.f;
-    }
-  };
-  auto stash = [&]() {
+  for (int t = 0; t < F::J2; ++t) {
+    const int e = (wave + t * NDY) * 64 + lane;
+    const int gy = y0 + dyb - D + e / C2, gx = x0 - D + e % C2;
+    const bool ok = e < F::R2 * C2 && (unsigned)gy < (unsigned)H && (unsigned)gx < (unsigned)W;
+    vo2[t] = ok ? (gy * W + gx) * 4 : kOffImage;
+  }
+  auto dma_stage = [&](int c0, float* img) {
 #pragma unroll
-    for (int k = 0; k < L1; ++k) {
-      const int e = tid + k * NT;
-      if (e < N1) s1[e] = r1[k];
-    }
+    for (int c = 0; c < CC; ++c) {
+      const bool cv = c0 + c < C;
+      const auto r1 = plane_rsrc(x1b + (size_t)(c0 + c) * HW, cv, HW * 4);
+      const auto r2 = plane_rsrc(x2b + (size_t)(c0 + c) * HW, cv, HW * 4);
 #pragma unroll
-    for (int k = 0; k < L2; ++k) {
-      const int e = tid + k * NT;
-      const int c = e / (R2 * C2);
-      const int rem = e - c * (R2 * C2);
-      const int rr = rem / C2, cc = rem - (rem / C2) * C2;
-      if (e < N2) s2[c * (R2 * XS) + rr * XS + cc] = r2[k];
+      for (int t = 0; t < F::J1; ++t)
+        if (wave + t * NDY < F::CH1) dma64(r1, img + c * P1 + (wave + t * NDY) * 64, vo1[t]);
+#pragma unroll
+      for (int t = 0; t < F::J2; ++t)
+        if (wave + t * NDY < F::CH2)
+          dma64(r2, img + CC * P1 + c * P2 + (wave + t * NDY) * 64, vo2[t]);
     }
   };
 
@@ -136,41 +153,29 @@ __global__ __launch_bounds__(64 * NDY) void corr_fwd_kernel(const float* __restr
 #pragma unroll
     for (int i = 0; i < PX; ++i) acc[j][i] = 0.f;
 
-  fetch(0);
-  stash();
+  dma_stage(0, sm);
+  dma_wait_all();
   __syncthreads();
-  for (int c0 = 0; c0 < C; c0 += CC) {
-    const bool more = c0 + CC < C;
-    if (more) fetch(c0 + CC);  // in flight during this stage's FMAs
+  int st = 0;
+  for (int c0 = 0; c0 < C; c0 += CC, ++st) {
+    const float* cur = sm + (st & 1) * STAGE;
+    if (c0 + CC < C) dma_stage(c0 + CC, sm + ((st + 1) & 1) * STAGE);  // in flight during FMAs
     if (active) {
+      const float* p1 = cur + r * TW + q * PX;
+      const float* p2 = cur + CC * P1 + (r + wave) * C2 + q * PX;
 #pragma unroll 2
       for (int c = 0; c < CC; ++c) {
         float a[PX], w[WIN];
-        const float4* p1 =
-            reinterpret_cast<const float4*>(s1 + c * (TH * TW) + r * TW + q * PX);
-#pragma unroll
-        for (int i = 0; i < PX / 4; ++i) {
-          const float4 t = p1[i];
-          a[4 * i] = t.x; a[4 * i + 1] = t.y; a[4 * i + 2] = t.z; a[4 * i + 3] = t.w;
-        }
-        const float4* p2 =
-            reinterpret_cast<const float4*>(s2 + c * (R2 * XS) + (r + wave) * XS + q * PX);
-#pragma unroll
-        for (int i = 0; i < WIN / 4; ++i) {
-          const float4 t = p2[i];
-          w[4 * i] = t.x; w[4 * i + 1] = t.y; w[4 * i + 2] = t.z; w[4 * i + 3] = t.w;
-        }
+        lds_read(p1 + c * P1, a);
+        lds_read(p2 + c * P2, w);
 #pragma unroll
         for (int dx = 0; dx < K; ++dx)
 #pragma unroll
           for (int i = 0; i < PX; ++i) acc[dx][i] = fmaf(a[i], w[i + dx], acc[dx][i]);
       }
     }
+    dma_wait_all();
     __syncthreads();
-    if (more) {
-      stash();
-      __syncthreads();
-    }
   }
 
   if (!active) return;
@@ -209,26 +214,24 @@ hipError_t launch_fwd(const float* x1, const float* x2, float* out, int B, int C
   return hipGetLastError();
 }
 
-// Tuning hook: usf_set_variant(op, i) forces candidate i for d=4
+// Tuning hook: usf_set_variant(0, i) forces candidate i for d=4
 // (tools/kbench.py sweeps them on the GPU); -1 = the shape heuristic below.
-
 hipError_t fwd_candidate_d4(int i, const float* x1, const float* x2, float* out, int B, int C,
                             int H, int W, hipStream_t s) {
   switch (i) {
-    case 0: return launch_fwd<4, 8, 8, 9, 4>(x1, x2, out, B, C, H, W, s);
-    case 1: return launch_fwd<4, 4, 8, 9, 8>(x1, x2, out, B, C, H, W, s);
-    case 2: return launch_fwd<4, 4, 8, 3, 8>(x1, x2, out, B, C, H, W, s);
-    case 3: return launch_fwd<4, 8, 8, 3, 4>(x1, x2, out, B, C, H, W, s);
-    case 4: return launch_fwd<4, 4, 16, 3, 8>(x1, x2, out, B, C, H, W, s);
-    case 5: return launch_fwd<4, 4, 16, 9, 8>(x1, x2, out, B, C, H, W, s);
-    case 6: return launch_fwd<4, 8, 8, 1, 8>(x1, x2, out, B, C, H, W, s);
-    case 7: return launch_fwd<4, 4, 8, 1, 8>(x1, x2, out, B, C, H, W, s);
-    case 8: return launch_fwd<4, 4, 4, 3, 8>(x1, x2, out, B, C, H, W, s);
-    case 9: return launch_fwd<4, 4, 8, 3, 16>(x1, x2, out, B, C, H, W, s);
+    case 0: return launch_fwd<4, 8, 8, 9, 8>(x1, x2, out, B, C, H, W, s);
+    case 1: return launch_fwd<4, 8, 8, 9, 4>(x1, x2, out, B, C, H, W, s);
+    case 2: return launch_fwd<4, 4, 8, 9, 8>(x1, x2, out, B, C, H, W, s);
+    case 3: return launch_fwd<4, 4, 8, 9, 16>(x1, x2, out, B, C, H, W, s);
+    case 4: return launch_fwd<4, 4, 8, 3, 8>(x1, x2, out, B, C, H, W, s);
+    case 5: return launch_fwd<4, 4, 8, 3, 16>(x1, x2, out, B, C, H, W, s);
+    case 6: return launch_fwd<4, 4, 16, 9, 8>(x1, x2, out, B, C, H, W, s);
+    case 7: return launch_fwd<4, 4, 16, 3, 8>(x1, x2, out, B, C, H, W, s);
+    case 8: return launch_fwd<4, 8, 8, 3, 8>(x1, x2, out, B, C, H, W, s);
     default: return hipErrorInvalidValue;
   }
 }
-constexpr int kFwdCandidates = 10;
+constexpr int kFwdCandidates = 9;
 
 template <int D>
 hipError_t fwd_dispatch(const float* x1, const float* x2, float* out, int B, int C, int H,
@@ -238,11 +241,11 @@ hipError_t fwd_dispatch(const float* x1, const float* x2, float* out, int B, int
     const int forced = variant_override(0);
     if (forced >= 0) return fwd_candidate_d4(forced, x1, x2, out, B, C, H, W, s);
   }
-  // Prefer the big tile (8 px/lane, one workgroup covers every displacement
-  // row: x1/x2 staged once); fall back to smaller tiles / split displacement
-  // rows when that would leave most of the 256 CUs idle.
+  // Prefer the big tile (8 px/lane, all displacement rows in one workgroup:
+  // x1/x2 staged once); fall back to smaller tiles / split displacement rows
+  // when that would leave most of the 256 CUs idle.
   const long big = (long)B * ((W + 63) / 64) * ((H + 7) / 8);
-  if (big >= 256) return launch_fwd<D, 8, 8, K, 4>(x1, x2, out, B, C, H, W, s);
+  if (big >= 256) return launch_fwd<D, 8, 8, K, 8>(x1, x2, out, B, C, H, W, s);
   const long mid = (long)B * ((W + 31) / 32) * ((H + 7) / 8);
   if (mid >= 256) return launch_fwd<D, 4, 8, K, 8>(x1, x2, out, B, C, H, W, s);
   return launch_fwd<D, 4, 8, 3, 8>(x1, x2, out, B, C, H, W, s);
@@ -255,13 +258,16 @@ struct BwdCfg {
   static constexpr int TW = SEGX * PX;
   static constexpr int TH = 64 / SEGX;
   static constexpr int NT = 64 * NW;
-  static constexpr int R = TH + 2 * D;           // staged rows
-  static constexpr int C2 = TW + 2 * D;          // staged cols
+  static constexpr int DYW = (K + NW - 1) / NW;      // displacement rows per wave
+  static constexpr int R = TH + 2 * D;               // staged rows
+  static constexpr int C2 = round_up(TW + 2 * D, 4);  // staged cols (row stride)
+  static constexpr int P = round_up(R * C2, 64);     // plane image (floats)
+  static constexpr int CH = P / 64;
+  static constexpr int J = (CH + NW - 1) / NW;       // chunks per wave per plane
   static constexpr int WIN = round_up(PX + 2 * D, 4);
-  static constexpr int XS = round_up(C2, 4) + 4;
-  static constexpr int SN = CC * R * XS + WIN;   // staging image
-  static constexpr int RN = NW * CC * TH * TW;   // per-wave partial sums (aliases staging)
-  static constexpr int SMN = SN > RN ? SN : RN;
+  static constexpr int XIMG = CC * P;
+  static constexpr int RED = NW * CC * TH * TW;      // per-wave partial sums
+  static constexpr int LDSN = 2 * XIMG + WIN + RED;
   static_assert(PX % 4 == 0, "PX must be a multiple of 4");
 };
 
@@ -270,17 +276,19 @@ template <int D, int PX, int SEGX, int NW, int CC, bool G2>
 __global__ __launch_bounds__(64 * NW) void corr_bwd_kernel(const float* __restrict__ xs,
                                                            const float* __restrict__ g,
                                                            float* __restrict__ gx, int C, int H,
-                                                           int W, int tiles_x) {
+                                                           int W, int tiles_x, int cg) {
   using F = BwdCfg<D, PX, SEGX, NW, CC>;
-  constexpr int K = F::K, TW = F::TW, TH = F::TH, NT = F::NT, R = F::R, C2 = F::C2;
-  constexpr int WIN = F::WIN, XS = F::XS;
-  __shared__ __attribute__((aligned(16))) float sm[F::SMN];
+  constexpr int K = F::K, TW = F::TW, TH = F::TH, NT = F::NT, C2 = F::C2, P = F::P;
+  constexpr int WIN = F::WIN, DYW = F::DYW, XIMG = F::XIMG;
+  __shared__ __attribute__((aligned(16))) float sm[F::LDSN];
+  float* red = sm + 2 * XIMG + WIN;
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
-  const int wave = tid >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int tile = blockIdx.x;
-  const int c0 = blockIdx.y * CC;
+  const int cbeg = blockIdx.y * cg;
+  const int cend = min(C, cbeg + cg);
   const int b = blockIdx.z;
   const int ty = tile / tiles_x;
   const int tx = tile - ty * tiles_x;
@@ -293,127 +301,108 @@ __global__ __launch_bounds__(64 * NW) void corr_bwd_kernel(const float* __restri
   const float* xsb = xs + (size_t)b * C * HW;
   const float* gb = g + (size_t)b * K * K * HW;
 
-  // stage xs rows [y0-D, y0+TH+D) x cols [x0-D, x0+TW+D) for CC channels:
-  // all loads in flight first (clamped unconditional loads), then LDS writes
-  {
-    constexpr int N = CC * R * C2, L = (N + NT - 1) / NT;
-    constexpr int CH = 16;  // loads in flight per batch (caps the staging registers)
-#pragma unroll 1
-    for (int k0 = 0; k0 < L; k0 += CH) {
-      float v[CH];
+  // this wave's DYW rows of g for its PX pixels, read once (clamped unconditional loads)
+  float gv[DYW][K][PX];
 #pragma unroll
-      for (int j = 0; j < CH; ++j) {
-        const int e = tid + (k0 + j) * NT;
-        const int c = e / (R * C2);
-        const int rem = e - c * (R * C2);
-        const int rr = rem / C2, cc = rem - (rem / C2) * C2;
-        const int gy = y0 - D + rr, gxx = x0 - D + cc;
-        const bool ok = e < N && c0 + c < C && (unsigned)gy < (unsigned)H && (unsigned)gxx < (unsigned)W;
-        const float t = xsb[ok ? (c0 + c) * HW + gy * W + gxx : 0];
-        v[j] = ok ? t : 0.f;
-      }
+  for (int t = 0; t < DYW; ++t) {
+    const int dy = wave * DYW + t;
 #pragma unroll
-      for (int j = 0; j < CH; ++j) {
-        const int e = tid + (k0 + j) * NT;
-        const int c = e / (R * C2);
-        const int rem = e - c * (R * C2);
-        const int rr = rem / C2, cc = rem - (rem / C2) * C2;
-        if (e < N) sm[c * (R * XS) + rr * XS + cc] = v[j];
+    for (int dx = 0; dx < K; ++dx) {
+      const int k = min(dy, K - 1) * K + dx;
+      const int yy = G2 ? y - dy + D : y;
+#pragma unroll
+      for (int i = 0; i < PX; ++i) {
+        const int xx = G2 ? xb + i - dx + D : xb + i;
+        const bool ok = dy < K && (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W;
+        const float v = gb[k * HW + (ok ? yy * W + xx : 0)];
+        gv[t][dx][i] = ok ? v : 0.f;
       }
     }
   }
-  __syncthreads();
 
-  float acc[CC][PX];
+  int vo[F::J];
 #pragma unroll
-  for (int c = 0; c < CC; ++c)
-#pragma unroll
-    for (int i = 0; i < PX; ++i) acc[c][i] = 0.f;
-
-  for (int dy = wave; dy < K; dy += NW) {
-    float gv[K][PX];
-    if (!G2) {
-      // g at the output pixels themselves: g[b, dy*K+dx, y, xb+i]
-      const bool rowok = y < H;
-#pragma unroll
-      for (int dx = 0; dx < K; ++dx) {
-        const float* gp = gb + (dy * K + dx) * HW + y * W + xb;
-#pragma unroll
-        for (int i = 0; i < PX; ++i) {
-          const bool ok = rowok && xb + i < W;
-          const float t = gp[ok ? i : 0 - (y * W + xb)];  // clamped to the plane start
-          gv[dx][i] = ok ? t : 0.f;
-        }
-      }
-    } else {
-      // g at the source pixels: g[b, dy*K+dx, y-(dy-D), xb+i-(dx-D)]
-      const int yy = y - dy + D;
-      const bool rowok = (unsigned)yy < (unsigned)H;
-#pragma unroll
-      for (int dx = 0; dx < K; ++dx) {
-        const int xx0 = xb - dx + D;
-        const float* gp = gb + (dy * K + dx) * HW + yy * W + xx0;
-#pragma unroll
-        for (int i = 0; i < PX; ++i) {
-          const bool ok = rowok && (unsigned)(xx0 + i) < (unsigned)W;
-          const float t = gp[ok ? i : 0 - (yy * W + xx0)];  // clamped to the plane start
-          gv[dx][i] = ok ? t : 0.f;
-        }
-      }
-    }
-    const int rs = G2 ? (2 * D - dy) : dy;
-    const float* srow = sm + (r + rs) * XS + q * PX;
+  for (int t = 0; t < F::J; ++t) {
+    const int e = (wave + t * NW) * 64 + lane;
+    const int gy = y0 - D + e / C2, gxx = x0 - D + e % C2;
+    const bool ok = e < F::R * C2 && (unsigned)gy < (unsigned)H && (unsigned)gxx < (unsigned)W;
+    vo[t] = ok ? (gy * W + gxx) * 4 : kOffImage;
+  }
+  auto dma_stage = [&](int c0, float* img) {
 #pragma unroll
     for (int c = 0; c < CC; ++c) {
-      float w[WIN];
-      const float4* p = reinterpret_cast<const float4*>(srow + c * (R * XS));
+      const auto rs = plane_rsrc(xsb + (size_t)(c0 + c) * HW, c0 + c < cend, HW * 4);
 #pragma unroll
-      for (int i = 0; i < WIN / 4; ++i) {
-        const float4 t = p[i];
-        w[4 * i] = t.x; w[4 * i + 1] = t.y; w[4 * i + 2] = t.z; w[4 * i + 3] = t.w;
-      }
-#pragma unroll
-      for (int dx = 0; dx < K; ++dx) {
-        const int cs = G2 ? (2 * D - dx) : dx;
-#pragma unroll
-        for (int i = 0; i < PX; ++i) acc[c][i] = fmaf(gv[dx][i], w[i + cs], acc[c][i]);
-      }
+      for (int t = 0; t < F::J; ++t)
+        if (wave + t * NW < F::CH) dma64(rs, img + c * P + (wave + t * NW) * 64, vo[t]);
     }
-  }
-  __syncthreads();  // every wave is done reading the staging image
-
-  float* rp = sm + wave * (CC * TH * TW) + r * TW + q * PX;
-#pragma unroll
-  for (int c = 0; c < CC; ++c)
-#pragma unroll
-    for (int i = 0; i < PX / 4; ++i)
-      reinterpret_cast<float4*>(rp + c * (TH * TW))[i] =
-          make_float4(acc[c][4 * i], acc[c][4 * i + 1], acc[c][4 * i + 2], acc[c][4 * i + 3]);
-  __syncthreads();
+  };
 
   const float cf = (float)C;
   float* gxb = gx + (size_t)b * C * HW;
-  for (int o = tid; o < CC * TH * TW; o += NT) {
-    float sum = 0.f;
+  dma_stage(cbeg, sm);
+  dma_wait_all();
+  __syncthreads();
+  int st = 0;
+  for (int c0 = cbeg; c0 < cend; c0 += CC, ++st) {
+    const float* cur = sm + (st & 1) * XIMG;
+    if (c0 + CC < cend) dma_stage(c0 + CC, sm + ((st + 1) & 1) * XIMG);
+    float* rp = red + wave * (CC * TH * TW) + r * TW + q * PX;
+#pragma unroll 2
+    for (int c = 0; c < CC; ++c) {
+      float acc[PX];
 #pragma unroll
-    for (int w = 0; w < NW; ++w) sum += sm[w * (CC * TH * TW) + o];
-    const int c = o / (TH * TW);
-    const int pix = o - c * (TH * TW);
-    const int yy = y0 + pix / TW;
-    const int xx = x0 + pix % TW;
-    if (c0 + c < C && yy < H && xx < W) gxb[(c0 + c) * HW + yy * W + xx] = sum / cf;
+      for (int i = 0; i < PX; ++i) acc[i] = 0.f;
+#pragma unroll
+      for (int t = 0; t < DYW; ++t) {
+        const int dy = wave * DYW + t;
+        if (dy < K) {
+          const int rs = G2 ? (2 * D - dy) : dy;
+          float w[WIN];
+          lds_read(cur + c * P + (r + rs) * C2 + q * PX, w);
+#pragma unroll
+          for (int dx = 0; dx < K; ++dx) {
+            const int cs = G2 ? (2 * D - dx) : dx;
+#pragma unroll
+            for (int i = 0; i < PX; ++i) acc[i] = fmaf(gv[t][dx][i], w[i + cs], acc[i]);
+          }
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < PX / 4; ++i)
+        reinterpret_cast<float4*>(rp + c * (TH * TW))[i] =
+            make_float4(acc[4 * i], acc[4 * i + 1], acc[4 * i + 2], acc[4 * i + 3]);
+    }
+    dma_wait_all();
+    __syncthreads();  // partials complete; next stage's image landed
+    for (int o = tid; o < CC * TH * TW; o += NT) {
+      float sum = 0.f;
+#pragma unroll
+      for (int w2 = 0; w2 < NW; ++w2) sum += red[w2 * (CC * TH * TW) + o];  // fixed order
+      const int c = o / (TH * TW);
+      const int pix = o - c * (TH * TW);
+      const int yy = y0 + pix / TW, xx = x0 + pix % TW;
+      if (c0 + c < cend && yy < H && xx < W) gxb[(c0 + c) * HW + yy * W + xx] = sum / cf;
+    }
+    __syncthreads();  // partial slices free for the next stage
   }
 }
 
-template <int D, bool G2, int PX = 4, int SEGX = 8, int NW = 3, int CC = 16>
+template <int D, bool G2, int PX = 4, int SEGX = 8, int NW = 3, int CC = 8>
 hipError_t launch_bwd(const float* xs, const float* g, float* gx, int B, int C, int H, int W,
                       hipStream_t s) {
   using F = BwdCfg<D, PX, SEGX, NW, CC>;
   const int tiles_x = (W + F::TW - 1) / F::TW;
   const int tiles_y = (H + F::TH - 1) / F::TH;
-  dim3 grid(tiles_x * tiles_y, (C + CC - 1) / CC, B);
+  const long tiles = (long)tiles_x * tiles_y * B;
+  // channel group per workgroup: g is re-read once per group, so use as few
+  // groups as still give ~512 workgroups
+  int groups = (int)((512 + tiles - 1) / tiles);
+  groups = max(1, min(groups, (C + CC - 1) / CC));
+  const int cg = round_up((C + groups - 1) / groups, CC);
+  dim3 grid(tiles_x * tiles_y, (C + cg - 1) / cg, B);
   hipLaunchKernelGGL((corr_bwd_kernel<D, PX, SEGX, NW, CC, G2>), grid, dim3(F::NT), 0, s, xs, g,
-                     gx, C, H, W, tiles_x);
+                     gx, C, H, W, tiles_x, cg);
   return hipGetLastError();
 }
 
@@ -421,12 +410,12 @@ template <bool G2>
 hipError_t bwd_candidate_d4(int i, const float* xs, const float* g, float* gx, int B, int C, int H,
                             int W, hipStream_t s) {
   switch (i) {
-    case 0: return launch_bwd<4, G2, 4, 8, 3, 16>(xs, g, gx, B, C, H, W, s);
-    case 1: return launch_bwd<4, G2, 4, 8, 3, 8>(xs, g, gx, B, C, H, W, s);
-    case 2: return launch_bwd<4, G2, 4, 16, 3, 16>(xs, g, gx, B, C, H, W, s);
-    case 3: return launch_bwd<4, G2, 4, 4, 3, 16>(xs, g, gx, B, C, H, W, s);
+    case 0: return launch_bwd<4, G2, 4, 8, 3, 8>(xs, g, gx, B, C, H, W, s);
+    case 1: return launch_bwd<4, G2, 4, 8, 3, 4>(xs, g, gx, B, C, H, W, s);
+    case 2: return launch_bwd<4, G2, 4, 8, 3, 16>(xs, g, gx, B, C, H, W, s);
+    case 3: return launch_bwd<4, G2, 4, 16, 3, 8>(xs, g, gx, B, C, H, W, s);
     case 4: return launch_bwd<4, G2, 4, 8, 9, 8>(xs, g, gx, B, C, H, W, s);
-    case 5: return launch_bwd<4, G2, 4, 8, 1, 16>(xs, g, gx, B, C, H, W, s);
+    case 5: return launch_bwd<4, G2, 4, 4, 3, 8>(xs, g, gx, B, C, H, W, s);
     default: return hipErrorInvalidValue;
   }
 }
