@@ -1,0 +1,41 @@
+"""Launch each hot-path kernel N times at PWCLite's B=8 KITTI call-site shapes,
+plain (no graphs) so rocprofv3 --pmc attributes counters per dispatch.
+Usage: rocprofv3 --pmc <counters> --kernel-trace --output-format csv -d DIR -o run -- python3 tools/kprof.py
+"""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+from unsamflow_amd import _lib  # noqa: E402
+from unsamflow_amd.kernel_timer import site_launcher  # noqa: E402
+
+SITES = [
+    ("corr_fwd", (8, 32, 64, 208)), ("corr_bwd", (8, 32, 64, 208, True, True)),
+    ("corr_fwd", (8, 64, 32, 104)), ("corr_bwd", (8, 64, 32, 104, True, True)),
+    ("corr_fwd", (8, 192, 4, 13)), ("corr_bwd", (8, 192, 4, 13, True, True)),
+    ("warp_bwd", (8, 32, 64, 208, "border", True, True)), ("warp_fwd", (8, 32, 64, 208, "border")),
+    ("warp_bwd", (8, 3, 256, 832, "border", False, True)),
+]
+
+
+def main():
+    _lib.load()
+    dev = torch.device("cuda:0")
+    n = int(os.environ.get("KPROF_N", "3"))
+    # calibration: a plain 256 MiB device copy (16-B loads/stores) for FETCH/WRITE_SIZE scaling
+    a = torch.empty(64 * 1024 * 1024, device=dev)
+    b = torch.empty_like(a)
+    for _ in range(n):
+        b.copy_(a)
+    for op, key in SITES:
+        fn = site_launcher(op, key, dev)
+        for _ in range(n):
+            fn()
+        torch.cuda.synchronize()
+    print("kprof done")
+
+
+if __name__ == "__main__":
+    main()
