@@ -58,15 +58,45 @@ __device__ __forceinline__ void dma64(__amdgpu_buffer_rsrc_t rsrc, float* dst, i
 
 __device__ __forceinline__ void dma_wait_all() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
-template <int N>
+// LDS read of N consecutive floats with ds_read_b64 (B64) or ds_read_b128.
+template <bool B64, int N>
 __device__ __forceinline__ void lds_read(const float* p, float (&v)[N]) {
-  static_assert(N % 4 == 0, "b128 reads");
+  if constexpr (B64) {
+    static_assert(N % 2 == 0, "b64 reads");
 #pragma unroll
-  for (int i = 0; i < N / 4; ++i) {
-    const float4 t = reinterpret_cast<const float4*>(p)[i];
-    v[4 * i] = t.x; v[4 * i + 1] = t.y; v[4 * i + 2] = t.z; v[4 * i + 3] = t.w;
+    for (int i = 0; i < N / 2; ++i) {
+      const float2 t = reinterpret_cast<const float2*>(p)[i];
+      v[2 * i] = t.x; v[2 * i + 1] = t.y;
+    }
+  } else {
+    static_assert(N % 4 == 0, "b128 reads");
+#pragma unroll
+    for (int i = 0; i < N / 4; ++i) {
+      const float4 t = reinterpret_cast<const float4*>(p)[i];
+      v[4 * i] = t.x; v[4 * i + 1] = t.y; v[4 * i + 2] = t.z; v[4 * i + 3] = t.w;
+    }
   }
 }
+
+// LDS layout policy, chosen with a model of gfx950's ds_read lane groups
+// (MI355X_MICROARCH.md §LDS; tools/lds_banks.py) so every window/segment read
+// is bank-conflict free:
+//  * PX == 8: lanes row-major (r = l / SEGX), ds_read_b64, row stride = TW+10
+//    floats (74 at TW=64): each 32-lane group of a b64 read covers all 64
+//    banks once.
+//  * PX == 4: lanes column-major (q = l / TH, r = l % TH), ds_read_b128, row
+//    stride = round_up(TW+2d, 16) + 8 (48 at TW=32).
+// Pad columns of an LDS row are DMA'd as out-of-range zeros.
+template <int PX, int SEGX, int D>
+struct Layout {
+  static constexpr int TW = SEGX * PX, TH = 64 / SEGX;
+  static constexpr bool B64 = PX == 8;
+  static constexpr bool COLMAJOR = PX != 8;
+  static constexpr int S = B64 ? TW + 10 : round_up(TW + 2 * D, 16) + 8;
+  static_assert(S >= TW + 2 * D, "row stride must hold the halo row");
+  __device__ static int row(int lane) { return COLMAJOR ? lane % TH : lane / SEGX; }
+  __device__ static int seg(int lane) { return COLMAJOR ? lane / TH : lane % SEGX; }
+};
 
 // ---------------------------------------------------------------- forward --
 template <int D, int PX, int SEGX, int NDY, int CC>
@@ -76,10 +106,12 @@ struct FwdCfg {
   static constexpr int TH = 64 / SEGX;              // tile height (rows)
   static constexpr int NT = 64 * NDY;               // threads per workgroup
   static constexpr int NDYG = (K + NDY - 1) / NDY;  // workgroups per tile
+  using L = Layout<PX, SEGX, D>;
   static constexpr int R2 = TH + NDY - 1;           // staged x2 rows
-  static constexpr int C2 = round_up(TW + 2 * D, 4);  // staged x2 cols (row stride)
-  static constexpr int P1 = TH * TW;                // x1 plane image (floats)
-  static constexpr int P2 = round_up(R2 * C2, 64);  // x2 plane image
+  static constexpr int C2 = TW + 2 * D;             // staged x2 cols
+  static constexpr int S = L::S;                    // LDS row stride (x1 and x2 images)
+  static constexpr int P1 = round_up(TH * S, 64);   // x1 plane image (floats)
+  static constexpr int P2 = round_up(R2 * S, 64);   // x2 plane image
   static constexpr int CH1 = P1 / 64, CH2 = P2 / 64;  // 64-float chunks per plane
   static constexpr int J1 = (CH1 + NDY - 1) / NDY;  // chunks per wave per plane
   static constexpr int J2 = (CH2 + NDY - 1) / NDY;
@@ -87,7 +119,7 @@ struct FwdCfg {
   static constexpr int STAGE = CC * (P1 + P2);
   static constexpr int LDSN = 2 * STAGE + WIN;      // two images + window over-read pad
   static_assert(PX % 4 == 0, "PX must be a multiple of 4 (ds_read_b128)");
-  static_assert(64 % SEGX == 0 && P1 % 64 == 0, "tile must be whole 64-float chunks");
+  static_assert(64 % SEGX == 0, "SEGX must divide 64");
 };
 
 template <int D, int PX, int SEGX, int NDY, int CC>
@@ -96,8 +128,9 @@ __global__ __launch_bounds__(64 * NDY) void corr_fwd_kernel(const float* __restr
                                                             float* __restrict__ out, int C,
                                                             int H, int W, int tiles_x) {
   using F = FwdCfg<D, PX, SEGX, NDY, CC>;
-  constexpr int K = F::K, TW = F::TW, TH = F::TH, C2 = F::C2, P1 = F::P1, P2 = F::P2;
+  constexpr int K = F::K, TW = F::TW, TH = F::TH, C2 = F::C2, S = F::S, P1 = F::P1, P2 = F::P2;
   constexpr int WIN = F::WIN, STAGE = F::STAGE;
+  constexpr bool B64 = F::L::B64;
   __shared__ __attribute__((aligned(16))) float sm[F::LDSN];
 
   const int lane = threadIdx.x & 63;
@@ -108,7 +141,7 @@ __global__ __launch_bounds__(64 * NDY) void corr_fwd_kernel(const float* __restr
   const int ty = tile / tiles_x;
   const int tx = tile - ty * tiles_x;
   const int y0 = ty * TH, x0 = tx * TW;
-  const int r = lane / SEGX, q = lane % SEGX;
+  const int r = F::L::row(lane), q = F::L::seg(lane);
   const int dy = dyb + wave;
   const bool active = dy < K;
 
@@ -116,19 +149,23 @@ __global__ __launch_bounds__(64 * NDY) void corr_fwd_kernel(const float* __restr
   const float* x1b = x1 + (size_t)b * C * HW;
   const float* x2b = x2 + (size_t)b * C * HW;
 
-  // stage-invariant per-lane byte offsets of this wave's chunks
+  // stage-invariant per-lane byte offsets of this wave's chunks (row stride S;
+  // pad columns and off-image pixels read as zeros)
   int vo1[F::J1], vo2[F::J2];
 #pragma unroll
   for (int t = 0; t < F::J1; ++t) {
     const int e = (wave + t * NDY) * 64 + lane;
-    const int gy = y0 + e / TW, gx = x0 + e % TW;
-    vo1[t] = (gy < H && gx < W) ? (gy * W + gx) * 4 : kOffImage;
+    const int rr = e / S, cc = e % S;
+    const int gy = y0 + rr, gx = x0 + cc;
+    const bool ok = rr < TH && cc < TW && gy < H && gx < W;
+    vo1[t] = ok ? (gy * W + gx) * 4 : kOffImage;
   }
 #pragma unroll
   for (int t = 0; t < F::J2; ++t) {
     const int e = (wave + t * NDY) * 64 + lane;
-    const int gy = y0 + dyb - D + e / C2, gx = x0 - D + e % C2;
-    const bool ok = e < F::R2 * C2 && (unsigned)gy < (unsigned)H && (unsigned)gx < (unsigned)W;
+    const int rr = e / S, cc = e % S;
+    const int gy = y0 + dyb - D + rr, gx = x0 - D + cc;
+    const bool ok = rr < F::R2 && cc < C2 && (unsigned)gy < (unsigned)H && (unsigned)gx < (unsigned)W;
     vo2[t] = ok ? (gy * W + gx) * 4 : kOffImage;
   }
   auto dma_stage = [&](int c0, float* img) {
@@ -161,13 +198,13 @@ __global__ __launch_bounds__(64 * NDY) void corr_fwd_kernel(const float* __restr
     const float* cur = sm + (st & 1) * STAGE;
     if (c0 + CC < C) dma_stage(c0 + CC, sm + ((st + 1) & 1) * STAGE);  // in flight during FMAs
     if (active) {
-      const float* p1 = cur + r * TW + q * PX;
-      const float* p2 = cur + CC * P1 + (r + wave) * C2 + q * PX;
+      const float* p1 = cur + r * S + q * PX;
+      const float* p2 = cur + CC * P1 + (r + wave) * S + q * PX;
 #pragma unroll 2
       for (int c = 0; c < CC; ++c) {
         float a[PX], w[WIN];
-        lds_read(p1 + c * P1, a);
-        lds_read(p2 + c * P2, w);
+        lds_read<B64>(p1 + c * P1, a);
+        lds_read<B64>(p2 + c * P2, w);
 #pragma unroll
         for (int dx = 0; dx < K; ++dx)
 #pragma unroll
@@ -222,16 +259,15 @@ hipError_t fwd_candidate_d4(int i, const float* x1, const float* x2, float* out,
     case 0: return launch_fwd<4, 8, 8, 9, 8>(x1, x2, out, B, C, H, W, s);
     case 1: return launch_fwd<4, 8, 8, 9, 4>(x1, x2, out, B, C, H, W, s);
     case 2: return launch_fwd<4, 4, 8, 9, 8>(x1, x2, out, B, C, H, W, s);
-    case 3: return launch_fwd<4, 4, 8, 9, 16>(x1, x2, out, B, C, H, W, s);
+    case 3: return launch_fwd<4, 4, 8, 9, 4>(x1, x2, out, B, C, H, W, s);
     case 4: return launch_fwd<4, 4, 8, 3, 8>(x1, x2, out, B, C, H, W, s);
-    case 5: return launch_fwd<4, 4, 8, 3, 16>(x1, x2, out, B, C, H, W, s);
-    case 6: return launch_fwd<4, 4, 16, 9, 8>(x1, x2, out, B, C, H, W, s);
-    case 7: return launch_fwd<4, 4, 16, 3, 8>(x1, x2, out, B, C, H, W, s);
-    case 8: return launch_fwd<4, 8, 8, 3, 8>(x1, x2, out, B, C, H, W, s);
+    case 5: return launch_fwd<4, 4, 8, 3, 4>(x1, x2, out, B, C, H, W, s);
+    case 6: return launch_fwd<4, 8, 8, 3, 4>(x1, x2, out, B, C, H, W, s);
+    case 7: return launch_fwd<4, 4, 8, 1, 8>(x1, x2, out, B, C, H, W, s);
     default: return hipErrorInvalidValue;
   }
 }
-constexpr int kFwdCandidates = 9;
+constexpr int kFwdCandidates = 8;
 
 template <int D>
 hipError_t fwd_dispatch(const float* x1, const float* x2, float* out, int B, int C, int H,
@@ -259,9 +295,11 @@ struct BwdCfg {
   static constexpr int TH = 64 / SEGX;
   static constexpr int NT = 64 * NW;
   static constexpr int DYW = (K + NW - 1) / NW;      // displacement rows per wave
+  using L = Layout<PX, SEGX, D>;
   static constexpr int R = TH + 2 * D;               // staged rows
-  static constexpr int C2 = round_up(TW + 2 * D, 4);  // staged cols (row stride)
-  static constexpr int P = round_up(R * C2, 64);     // plane image (floats)
+  static constexpr int C2 = TW + 2 * D;              // staged cols
+  static constexpr int S = L::S;                     // LDS row stride
+  static constexpr int P = round_up(R * S, 64);      // plane image (floats)
   static constexpr int CH = P / 64;
   static constexpr int J = (CH + NW - 1) / NW;       // chunks per wave per plane
   static constexpr int WIN = round_up(PX + 2 * D, 4);
@@ -278,8 +316,9 @@ __global__ __launch_bounds__(64 * NW) void corr_bwd_kernel(const float* __restri
                                                            float* __restrict__ gx, int C, int H,
                                                            int W, int tiles_x, int cg) {
   using F = BwdCfg<D, PX, SEGX, NW, CC>;
-  constexpr int K = F::K, TW = F::TW, TH = F::TH, NT = F::NT, C2 = F::C2, P = F::P;
+  constexpr int K = F::K, TW = F::TW, TH = F::TH, NT = F::NT, C2 = F::C2, S = F::S, P = F::P;
   constexpr int WIN = F::WIN, DYW = F::DYW, XIMG = F::XIMG;
+  constexpr bool B64 = F::L::B64;
   __shared__ __attribute__((aligned(16))) float sm[F::LDSN];
   float* red = sm + 2 * XIMG + WIN;
 
@@ -293,7 +332,7 @@ __global__ __launch_bounds__(64 * NW) void corr_bwd_kernel(const float* __restri
   const int ty = tile / tiles_x;
   const int tx = tile - ty * tiles_x;
   const int y0 = ty * TH, x0 = tx * TW;
-  const int r = lane / SEGX, q = lane % SEGX;
+  const int r = F::L::row(lane), q = F::L::seg(lane);
   const int y = y0 + r;
   const int xb = x0 + q * PX;
 
@@ -324,8 +363,9 @@ __global__ __launch_bounds__(64 * NW) void corr_bwd_kernel(const float* __restri
 #pragma unroll
   for (int t = 0; t < F::J; ++t) {
     const int e = (wave + t * NW) * 64 + lane;
-    const int gy = y0 - D + e / C2, gxx = x0 - D + e % C2;
-    const bool ok = e < F::R * C2 && (unsigned)gy < (unsigned)H && (unsigned)gxx < (unsigned)W;
+    const int rr = e / S, cc = e % S;
+    const int gy = y0 - D + rr, gxx = x0 - D + cc;
+    const bool ok = rr < F::R && cc < C2 && (unsigned)gy < (unsigned)H && (unsigned)gxx < (unsigned)W;
     vo[t] = ok ? (gy * W + gxx) * 4 : kOffImage;
   }
   auto dma_stage = [&](int c0, float* img) {
@@ -359,7 +399,7 @@ __global__ __launch_bounds__(64 * NW) void corr_bwd_kernel(const float* __restri
         if (dy < K) {
           const int rs = G2 ? (2 * D - dy) : dy;
           float w[WIN];
-          lds_read(cur + c * P + (r + rs) * C2 + q * PX, w);
+          lds_read<B64>(cur + c * P + (r + rs) * S + q * PX, w);
 #pragma unroll
           for (int dx = 0; dx < K; ++dx) {
             const int cs = G2 ? (2 * D - dx) : dx;
@@ -388,7 +428,7 @@ __global__ __launch_bounds__(64 * NW) void corr_bwd_kernel(const float* __restri
   }
 }
 
-template <int D, bool G2, int PX = 4, int SEGX = 8, int NW = 3, int CC = 8>
+template <int D, bool G2, int PX = 4, int SEGX = 8, int NW = 3, int CC = 4>
 hipError_t launch_bwd(const float* xs, const float* g, float* gx, int B, int C, int H, int W,
                       hipStream_t s) {
   using F = BwdCfg<D, PX, SEGX, NW, CC>;
@@ -410,16 +450,14 @@ template <bool G2>
 hipError_t bwd_candidate_d4(int i, const float* xs, const float* g, float* gx, int B, int C, int H,
                             int W, hipStream_t s) {
   switch (i) {
-    case 0: return launch_bwd<4, G2, 4, 8, 3, 8>(xs, g, gx, B, C, H, W, s);
-    case 1: return launch_bwd<4, G2, 4, 8, 3, 4>(xs, g, gx, B, C, H, W, s);
-    case 2: return launch_bwd<4, G2, 4, 8, 3, 16>(xs, g, gx, B, C, H, W, s);
-    case 3: return launch_bwd<4, G2, 4, 16, 3, 8>(xs, g, gx, B, C, H, W, s);
-    case 4: return launch_bwd<4, G2, 4, 8, 9, 8>(xs, g, gx, B, C, H, W, s);
-    case 5: return launch_bwd<4, G2, 4, 4, 3, 8>(xs, g, gx, B, C, H, W, s);
+    case 0: return launch_bwd<4, G2, 4, 8, 3, 4>(xs, g, gx, B, C, H, W, s);
+    case 1: return launch_bwd<4, G2, 4, 8, 3, 8>(xs, g, gx, B, C, H, W, s);
+    case 2: return launch_bwd<4, G2, 4, 8, 9, 4>(xs, g, gx, B, C, H, W, s);
+    case 3: return launch_bwd<4, G2, 4, 8, 9, 8>(xs, g, gx, B, C, H, W, s);
     default: return hipErrorInvalidValue;
   }
 }
-constexpr int kBwdCandidates = 6;
+constexpr int kBwdCandidates = 4;
 
 template <int D>
 hipError_t bwd_dispatch(const float* x1, const float* x2, const float* g, float* gx1, float* gx2,

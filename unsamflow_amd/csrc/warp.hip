@@ -22,12 +22,15 @@
 // and weights are computed once per lane and reused over its channels. grad_x uses fp32
 // global atomics (global_atomic_add_f32, no CAS loop); grad_flow is a
 // per-lane reduction over channels, written once (deterministic).
+#include <climits>
+
 #include "usf_common.h"
 
 namespace usf {
 namespace {
 
 struct Tap {
+  int xw, yn;                   // integer north-west corner (before masking)
   int o_nw, o_ne, o_sw, o_se;   // offsets within a channel plane
   bool m_nw, m_ne, m_sw, m_se;  // corner inside the image
   float n, s, w, e;             // distances (see header)
@@ -67,6 +70,8 @@ __device__ __forceinline__ Tap make_tap(float u, float v, int x, int y, int H, i
   t.s = 1.0f - t.n;
   const int xw = (int)fx, yn = (int)fy;
   const int xe = xw + 1, ys = yn + 1;
+  t.xw = xw;
+  t.yn = yn;
   const bool vxw = (unsigned)xw < (unsigned)W, vxe = (unsigned)xe < (unsigned)W;
   const bool vyn = (unsigned)yn < (unsigned)H, vys = (unsigned)ys < (unsigned)H;
   t.m_nw = vxw && vyn;
@@ -183,6 +188,138 @@ __global__ __launch_bounds__(256) void warp_bwd_kernel(const float* __restrict__
   }
 }
 
+// grad_x with the corner scatter pre-summed in LDS. A workgroup owns a 2-D
+// tile of TW x TH source pixels (TW*TH = 256/CS) x CS channel slices. With a
+// smooth flow the tile's 4*TW*TH*C corner targets fall in a small box; the
+// box is found by an LDS min/max reduction, zeroed in LDS, filled with
+// ds_add_f32 (LDS float atomics) and then flushed with ONE global atomic per
+// touched cell, row-contiguous across lanes: ~3-4x fewer global atomics than
+// one per corner. A tile whose box exceeds kAggCap floats (large or
+// discontinuous flow) falls back to direct global atomics. grad_flow (if
+// requested) is computed in the same channel loop and combined over the
+// slices in a fixed order, as in warp_bwd_kernel.
+constexpr int kAggCap = 8192;
+
+template <bool BORDER, bool WANT_GF, int CS>
+__global__ __launch_bounds__(256) void warp_bwd_gx_kernel(const float* __restrict__ x,
+                                                          const float* __restrict__ flow,
+                                                          long long fbs,
+                                                          const float* __restrict__ gout,
+                                                          float* __restrict__ gx,
+                                                          float* __restrict__ gflow, int B, int C,
+                                                          int H, int W, int tiles_x) {
+  constexpr int TPX = 256 / CS;
+  constexpr int TW = TPX >= 16 ? 16 : TPX;
+  constexpr int TH = TPX / TW;
+  __shared__ float agg[kAggCap];
+  __shared__ float red[2][256];
+  __shared__ int box[4];  // x lo, x hi, y lo, y hi of in-image corner targets
+  const int HW = H * W;
+  const int t = threadIdx.x;
+  const int slice = t / TPX;
+  const int pl = t - slice * TPX;
+  const int b = blockIdx.y;
+  const int ty = blockIdx.x / tiles_x;
+  const int tx = blockIdx.x - ty * tiles_x;
+  const int py = ty * TH + pl / TW, pxx = tx * TW + pl % TW;
+  const bool valid = py < H && pxx < W;
+  const int p = py * W + pxx;
+  Tap tp{};
+  if (valid) {
+    const float* fb = flow + b * fbs;
+    tp = make_tap(fb[p], fb[HW + p], pxx, py, H, W, BORDER);
+  }
+  if (t == 0) {
+    box[0] = INT_MAX; box[1] = INT_MIN; box[2] = INT_MAX; box[3] = INT_MIN;
+  }
+  __syncthreads();
+  const bool hit = valid && (tp.m_nw || tp.m_ne || tp.m_sw || tp.m_se);
+  if (slice == 0 && hit) {
+    atomicMin(&box[0], max(tp.xw, 0));
+    atomicMax(&box[1], min(tp.xw + 1, W - 1));
+    atomicMin(&box[2], max(tp.yn, 0));
+    atomicMax(&box[3], min(tp.yn + 1, H - 1));
+  }
+  __syncthreads();
+  const int bx0 = box[0], by0 = box[2];
+  const int bw = box[1] - bx0 + 1, bh = box[3] - by0 + 1;
+  const bool any = box[1] >= box[0];
+  const bool use_lds = any && (long)bw * bh * C <= kAggCap;  // block-uniform
+  const int area = use_lds ? bw * bh : 0;
+  if (use_lds) {
+    for (int i = t; i < C * area; i += 256) agg[i] = 0.f;
+    __syncthreads();
+  }
+
+  float dix = 0.f, diy = 0.f;
+  if (valid) {
+    const float wnw = tp.s * tp.e, wne = tp.s * tp.w, wsw = tp.n * tp.e, wse = tp.n * tp.w;
+    const float* xb = x + (size_t)b * C * HW;
+    const float* gb = gout + (size_t)b * C * HW + p;
+    float* gxb = gx + (size_t)b * C * HW;
+    // LDS offsets of the 4 corners inside the box (valid only when masked in)
+    const int lx = tp.xw - bx0, ly = tp.yn - by0;
+    const int a_nw = ly * bw + lx, a_ne = a_nw + 1, a_sw = a_nw + bw, a_se = a_sw + 1;
+#pragma unroll 4
+    for (int c = slice; c < C; c += CS) {
+      const float go = gb[(size_t)c * HW];
+      if (use_lds) {
+        float* ac = agg + c * area;
+        if (tp.m_nw) atomicAdd(ac + a_nw, go * wnw);
+        if (tp.m_ne) atomicAdd(ac + a_ne, go * wne);
+        if (tp.m_sw) atomicAdd(ac + a_sw, go * wsw);
+        if (tp.m_se) atomicAdd(ac + a_se, go * wse);
+      } else {
+        float* gc = gxb + (size_t)c * HW;
+        if (tp.m_nw) atomicAdd(gc + tp.o_nw, go * wnw);
+        if (tp.m_ne) atomicAdd(gc + tp.o_ne, go * wne);
+        if (tp.m_sw) atomicAdd(gc + tp.o_sw, go * wsw);
+        if (tp.m_se) atomicAdd(gc + tp.o_se, go * wse);
+      }
+      if (WANT_GF) {
+        const float* xc = xb + (size_t)c * HW;
+        const float vnw = tp.m_nw ? xc[tp.o_nw] : 0.f;
+        const float vne = tp.m_ne ? xc[tp.o_ne] : 0.f;
+        const float vsw = tp.m_sw ? xc[tp.o_sw] : 0.f;
+        const float vse = tp.m_se ? xc[tp.o_se] : 0.f;
+        dix += ((vne - vnw) * tp.s + (vse - vsw) * tp.n) * go;
+        diy += ((vsw - vnw) * tp.e + (vse - vne) * tp.w) * go;
+      }
+    }
+  }
+  if (use_lds) {
+    __syncthreads();
+    float* gxb = gx + (size_t)b * C * HW;
+    for (int i = t; i < C * area; i += 256) {
+      const float v = agg[i];
+      if (v != 0.f) {
+        const int c = i / area;
+        const int rem = i - c * area;
+        const int iy = rem / bw;
+        atomicAdd(gxb + (size_t)c * HW + (by0 + iy) * W + bx0 + (rem - iy * bw), v);
+      }
+    }
+  }
+  if (WANT_GF) {
+    if (CS > 1) {
+      red[0][t] = dix;
+      red[1][t] = diy;
+      __syncthreads();
+      if (slice != 0) return;
+#pragma unroll
+      for (int k = 1; k < CS; ++k) {
+        dix += red[0][pl + k * TPX];
+        diy += red[1][pl + k * TPX];
+      }
+    }
+    if (!valid) return;
+    const float ggx = dix * tp.mx, ggy = diy * tp.my;
+    float* gf = gflow + (size_t)b * 2 * HW + p;
+    gf[0] = (ggx / (float)(W - 1)) * 2.0f;
+    gf[HW] = (ggy / (float)(H - 1)) * 2.0f;
+  }
+}
+
 // Channel slices per workgroup: the smallest CS in {1,4,16,64} giving >= 1024
 // workgroups (8 XCDs x 32 CUs x 4), capped by C.
 inline int pick_cs(int B, int C, int HW) {
@@ -218,13 +355,17 @@ template <bool BORDER, int CS>
 void bwd_launch_cs(const float* x, const float* flow, long long fbs, const float* gout, float* gx,
                    float* gflow, int B, int C, int H, int W, hipStream_t s) {
   const dim3 grid((unsigned)((H * W + 256 / CS - 1) / (256 / CS)), (unsigned)B), block(256);
-  if (gx && gflow)
-    hipLaunchKernelGGL((warp_bwd_kernel<BORDER, true, true, CS>), grid, block, 0, s, x, flow, fbs,
-                       gout, gx, gflow, B, C, H, W);
-  else if (gx)
-    hipLaunchKernelGGL((warp_bwd_kernel<BORDER, true, false, CS>), grid, block, 0, s, x, flow,
-                       fbs, gout, gx, gflow, B, C, H, W);
-  else
+  if (gx) {
+    constexpr int TPX = 256 / CS, TW = TPX >= 16 ? 16 : TPX, TH = TPX / TW;
+    const int tiles_x = (W + TW - 1) / TW, tiles_y = (H + TH - 1) / TH;
+    const dim3 g2((unsigned)(tiles_x * tiles_y), (unsigned)B);
+    if (gflow)
+      hipLaunchKernelGGL((warp_bwd_gx_kernel<BORDER, true, CS>), g2, block, 0, s, x, flow, fbs,
+                         gout, gx, gflow, B, C, H, W, tiles_x);
+    else
+      hipLaunchKernelGGL((warp_bwd_gx_kernel<BORDER, false, CS>), g2, block, 0, s, x, flow, fbs,
+                         gout, gx, gflow, B, C, H, W, tiles_x);
+  } else
     hipLaunchKernelGGL((warp_bwd_kernel<BORDER, false, true, CS>), grid, block, 0, s, x, flow,
                        fbs, gout, gx, gflow, B, C, H, W);
 }
