@@ -61,12 +61,18 @@ def main():
                 print(res[-1], flush=True)
             lib.usf_set_variant(1, -1)
         if "warp" in a.ops and H > 4:
-            for key in [("warp_fwd", (B, C, H, W, "border")), ("warp_bwd", (B, C, H, W, "border", True, True))]:
-                op, k = key
-                us = device_time_us(site_launcher(op, k, dev))
-                nbytes = warp_bytes(B, C, H, W) if op == "warp_fwd" else warp_bytes(B, C, H, W, True)
-                res.append(dict(op=op, shape=list(k), us=round(us, 2), gbps=round(nbytes / us / 1e3, 1)))
+            k = (B, C, H, W, "border")
+            us = device_time_us(site_launcher("warp_fwd", k, dev))
+            res.append(dict(op="warp_fwd", shape=list(k), us=round(us, 2), gbps=round(warp_bytes(B, C, H, W) / us / 1e3, 1)))
+            print(res[-1], flush=True)
+            k = (B, C, H, W, "border", True, True)
+            for v in (-1, 0, 1):
+                lib.usf_set_variant(2, v)
+                us = device_time_us(site_launcher("warp_bwd", k, dev))
+                res.append(dict(op="warp_bwd", shape=list(k), variant=v, us=round(us, 2),
+                                gbps=round(warp_bytes(B, C, H, W, True) / us / 1e3, 1)))
                 print(res[-1], flush=True)
+            lib.usf_set_variant(2, -1)
     os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
     with open(a.out, "w") as f:
         json.dump(res, f, indent=1)

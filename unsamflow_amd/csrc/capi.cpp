@@ -165,7 +165,7 @@ int usf_warp_bwd_f32(const float* x, const float* flow, long long flow_bstride,
 
 int usf_set_variant(int op, int index) {
   clear_error();
-  if (op < 0 || op > 1 || index < -1 || index >= variant_count(op)) {
+  if (op < 0 || op > 2 || index < -1 || index >= variant_count(op)) {
     set_error("usf_set_variant: bad op %d / index %d", op, index);
     return USF_EINVAL;
   }

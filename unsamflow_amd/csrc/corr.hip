@@ -32,6 +32,8 @@
 //    in VGPRs for the whole channel loop (g read once per workgroup); per
 //    channel the DYW partial rows are summed in registers, the NW per-wave
 //    partials are added through LDS in a fixed order and written once.
+#include <cstdint>
+
 #include "usf_common.h"
 
 namespace usf {
@@ -76,6 +78,44 @@ __device__ __forceinline__ void lds_read(const float* p, float (&v)[N]) {
       v[4 * i] = t.x; v[4 * i + 1] = t.y; v[4 * i + 2] = t.z; v[4 * i + 3] = t.w;
     }
   }
+}
+
+using f2v = __attribute__((ext_vector_type(2))) float;
+
+// LDS byte address of a pointer into __shared__ memory.
+__device__ __forceinline__ unsigned lds_addr(const float* p) {
+  return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) float*)p;
+}
+
+// x1 segment (8 floats at pa) + x2 window (16 floats at pw) with twelve
+// ds_read_b64 in ONE asm statement that also waits for them: hipcc would
+// otherwise fuse adjacent b64 reads into ds_read2_b64, whose 16-lane groups
+// bank mod 32 and conflict on the stride-74 image (measured with
+// tools/probes/lds_probe.hip + SQ_LDS_BANK_CONFLICT).
+__device__ __forceinline__ void lds_read_px8(const float* pa, const float* pw, float (&a)[8],
+                                             float (&w)[16]) {
+  f2v a0, a1, a2, a3, w0, w1, w2, w3, w4, w5, w6, w7;
+  asm volatile(
+      "ds_read_b64 %0, %12\n\t"
+      "ds_read_b64 %1, %12 offset:8\n\t"
+      "ds_read_b64 %2, %12 offset:16\n\t"
+      "ds_read_b64 %3, %12 offset:24\n\t"
+      "ds_read_b64 %4, %13\n\t"
+      "ds_read_b64 %5, %13 offset:8\n\t"
+      "ds_read_b64 %6, %13 offset:16\n\t"
+      "ds_read_b64 %7, %13 offset:24\n\t"
+      "ds_read_b64 %8, %13 offset:32\n\t"
+      "ds_read_b64 %9, %13 offset:40\n\t"
+      "ds_read_b64 %10, %13 offset:48\n\t"
+      "ds_read_b64 %11, %13 offset:56\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(a0), "=&v"(a1), "=&v"(a2), "=&v"(a3), "=&v"(w0), "=&v"(w1), "=&v"(w2), "=&v"(w3),
+        "=&v"(w4), "=&v"(w5), "=&v"(w6), "=&v"(w7)
+      : "v"(lds_addr(pa)), "v"(lds_addr(pw))
+      : "memory");
+  a[0] = a0.x; a[1] = a0.y; a[2] = a1.x; a[3] = a1.y; a[4] = a2.x; a[5] = a2.y; a[6] = a3.x; a[7] = a3.y;
+  w[0] = w0.x; w[1] = w0.y; w[2] = w1.x; w[3] = w1.y; w[4] = w2.x; w[5] = w2.y; w[6] = w3.x; w[7] = w3.y;
+  w[8] = w4.x; w[9] = w4.y; w[10] = w5.x; w[11] = w5.y; w[12] = w6.x; w[13] = w6.y; w[14] = w7.x; w[15] = w7.y;
 }
 
 // LDS layout policy, chosen with a model of gfx950's ds_read lane groups
@@ -203,8 +243,12 @@ __global__ __launch_bounds__(64 * NDY) void corr_fwd_kernel(const float* __restr
 #pragma unroll 2
       for (int c = 0; c < CC; ++c) {
         float a[PX], w[WIN];
-        lds_read<B64>(p1 + c * P1, a);
-        lds_read<B64>(p2 + c * P2, w);
+        if constexpr (B64 && PX == 8 && WIN == 16) {
+          lds_read_px8(p1 + c * P1, p2 + c * P2, a, w);
+        } else {
+          lds_read<B64>(p1 + c * P1, a);
+          lds_read<B64>(p2 + c * P2, w);
+        }
 #pragma unroll
         for (int dx = 0; dx < K; ++dx)
 #pragma unroll
@@ -387,7 +431,8 @@ __global__ __launch_bounds__(64 * NW) void corr_bwd_kernel(const float* __restri
   for (int c0 = cbeg; c0 < cend; c0 += CC, ++st) {
     const float* cur = sm + (st & 1) * XIMG;
     if (c0 + CC < cend) dma_stage(c0 + CC, sm + ((st + 1) & 1) * XIMG);
-    float* rp = red + wave * (CC * TH * TW) + r * TW + q * PX;
+    // partials stored lane-linear (lane*PX): conflict-free ds_write_b128
+    float* rp = red + wave * (CC * TH * TW) + lane * PX;
 #pragma unroll 2
     for (int c = 0; c < CC; ++c) {
       float acc[PX];
@@ -416,12 +461,16 @@ __global__ __launch_bounds__(64 * NW) void corr_bwd_kernel(const float* __restri
     dma_wait_all();
     __syncthreads();  // partials complete; next stage's image landed
     for (int o = tid; o < CC * TH * TW; o += NT) {
-      float sum = 0.f;
-#pragma unroll
-      for (int w2 = 0; w2 < NW; ++w2) sum += red[w2 * (CC * TH * TW) + o];  // fixed order
       const int c = o / (TH * TW);
       const int pix = o - c * (TH * TW);
-      const int yy = y0 + pix / TW, xx = x0 + pix % TW;
+      const int py = pix / TW, pxo = pix % TW;
+      // lane that owns pixel (py, pxo) under the layout's lane mapping
+      const int ol = F::L::COLMAJOR ? (pxo / PX) * TH + py : py * SEGX + pxo / PX;
+      const int ridx = c * (TH * TW) + ol * PX + pxo % PX;
+      float sum = 0.f;
+#pragma unroll
+      for (int w2 = 0; w2 < NW; ++w2) sum += red[w2 * (CC * TH * TW) + ridx];  // fixed order
+      const int yy = y0 + py, xx = x0 + pxo;
       if (c0 + c < cend && yy < H && xx < W) gxb[(c0 + c) * HW + yy * W + xx] = sum / cf;
     }
     __syncthreads();  // partial slices free for the next stage
@@ -478,9 +527,9 @@ hipError_t bwd_dispatch(const float* x1, const float* x2, const float* g, float*
 
 }  // namespace
 
-static int g_variant[2] = {-1, -1};
+static int g_variant[3] = {-1, -1, -1};
 int variant_override(int op) { return __atomic_load_n(&g_variant[op], __ATOMIC_RELAXED); }
-int variant_count(int op) { return op == 0 ? kFwdCandidates : kBwdCandidates; }
+int variant_count(int op) { return op == 0 ? kFwdCandidates : op == 1 ? kBwdCandidates : 2; }
 void set_variant_override(int op, int index) { __atomic_store_n(&g_variant[op], index, __ATOMIC_RELAXED); }
 
 hipError_t corr_fwd_launch(const float* x1, const float* x2, float* out, int B, int C, int H,

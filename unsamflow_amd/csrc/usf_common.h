@@ -13,7 +13,7 @@ void clear_error();
 // Round n up to a multiple of m (compile-time helper).
 __host__ __device__ constexpr int round_up(int n, int m) { return ((n + m - 1) / m) * m; }
 
-// Tuning override of usf_set_variant (op 0: corr fwd, op 1: corr bwd; -1 = heuristic).
+// Tuning override of usf_set_variant (op 0: corr fwd, 1: corr bwd, 2: warp grad_x; -1 = default).
 int variant_override(int op);
 int variant_count(int op);
 void set_variant_override(int op, int index);

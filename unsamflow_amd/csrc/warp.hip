@@ -200,7 +200,7 @@ __global__ __launch_bounds__(256) void warp_bwd_kernel(const float* __restrict__
 // slices in a fixed order, as in warp_bwd_kernel.
 constexpr int kAggCap = 8192;
 
-template <bool BORDER, bool WANT_GF, int CS>
+template <bool BORDER, bool WANT_GF, int CS, bool LDS_AGG>
 __global__ __launch_bounds__(256) void warp_bwd_gx_kernel(const float* __restrict__ x,
                                                           const float* __restrict__ flow,
                                                           long long fbs,
@@ -233,18 +233,31 @@ __global__ __launch_bounds__(256) void warp_bwd_gx_kernel(const float* __restric
     box[0] = INT_MAX; box[1] = INT_MIN; box[2] = INT_MAX; box[3] = INT_MIN;
   }
   __syncthreads();
-  const bool hit = valid && (tp.m_nw || tp.m_ne || tp.m_sw || tp.m_se);
-  if (slice == 0 && hit) {
-    atomicMin(&box[0], max(tp.xw, 0));
-    atomicMax(&box[1], min(tp.xw + 1, W - 1));
-    atomicMin(&box[2], max(tp.yn, 0));
-    atomicMax(&box[3], min(tp.yn + 1, H - 1));
+  {
+    // wave-level min/max with shuffles, then one LDS atomic per wave (a
+    // same-address LDS atomic from every lane serialises 64-fold)
+    const bool hit = valid && slice == 0 && (tp.m_nw || tp.m_ne || tp.m_sw || tp.m_se);
+    int xl = hit ? max(tp.xw, 0) : INT_MAX, xh = hit ? min(tp.xw + 1, W - 1) : INT_MIN;
+    int yl = hit ? max(tp.yn, 0) : INT_MAX, yh = hit ? min(tp.yn + 1, H - 1) : INT_MIN;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      xl = min(xl, __shfl_xor(xl, off));
+      xh = max(xh, __shfl_xor(xh, off));
+      yl = min(yl, __shfl_xor(yl, off));
+      yh = max(yh, __shfl_xor(yh, off));
+    }
+    if ((t & 63) == 0 && xh >= xl) {
+      atomicMin(&box[0], xl);
+      atomicMax(&box[1], xh);
+      atomicMin(&box[2], yl);
+      atomicMax(&box[3], yh);
+    }
   }
   __syncthreads();
   const int bx0 = box[0], by0 = box[2];
   const int bw = box[1] - bx0 + 1, bh = box[3] - by0 + 1;
   const bool any = box[1] >= box[0];
-  const bool use_lds = any && (long)bw * bh * C <= kAggCap;  // block-uniform
+  const bool use_lds = LDS_AGG && any && (long)bw * bh * C <= kAggCap;  // block-uniform
   const int area = use_lds ? bw * bh : 0;
   if (use_lds) {
     for (int i = t; i < C * area; i += 256) agg[i] = 0.f;
@@ -289,14 +302,17 @@ __global__ __launch_bounds__(256) void warp_bwd_gx_kernel(const float* __restric
   }
   if (use_lds) {
     __syncthreads();
-    float* gxb = gx + (size_t)b * C * HW;
-    for (int i = t; i < C * area; i += 256) {
-      const float v = agg[i];
-      if (v != 0.f) {
-        const int c = i / area;
-        const int rem = i - c * area;
-        const int iy = rem / bw;
-        atomicAdd(gxb + (size_t)c * HW + (by0 + iy) * W + bx0 + (rem - iy * bw), v);
+    // flush row by row: lanes run along the box row (contiguous global
+    // addresses); one global atomic per touched cell
+    float* gxb = gx + (size_t)b * C * HW + by0 * W + bx0;
+    const int nrows = C * bh;
+    for (int row = t / 64; row < nrows; row += 4) {
+      const int c = row / bh, iy = row - (row / bh) * bh;
+      const float* src = agg + row * bw;
+      float* dst = gxb + (size_t)c * HW + iy * W;
+      for (int ix = t & 63; ix < bw; ix += 64) {
+        const float v = src[ix];
+        if (v != 0.f) atomicAdd(dst + ix, v);
       }
     }
   }
@@ -359,12 +375,20 @@ void bwd_launch_cs(const float* x, const float* flow, long long fbs, const float
     constexpr int TPX = 256 / CS, TW = TPX >= 16 ? 16 : TPX, TH = TPX / TW;
     const int tiles_x = (W + TW - 1) / TW, tiles_y = (H + TH - 1) / TH;
     const dim3 g2((unsigned)(tiles_x * tiles_y), (unsigned)B);
-    if (gflow)
-      hipLaunchKernelGGL((warp_bwd_gx_kernel<BORDER, true, CS>), g2, block, 0, s, x, flow, fbs,
-                         gout, gx, gflow, B, C, H, W, tiles_x);
+    // usf_set_variant(2, v): 0 = LDS-aggregated scatter, 1 = direct global atomics
+    const bool agg = variant_override(2) != 1;
+    if (gflow && agg)
+      hipLaunchKernelGGL((warp_bwd_gx_kernel<BORDER, true, CS, true>), g2, block, 0, s, x, flow,
+                         fbs, gout, gx, gflow, B, C, H, W, tiles_x);
+    else if (gflow)
+      hipLaunchKernelGGL((warp_bwd_gx_kernel<BORDER, true, CS, false>), g2, block, 0, s, x, flow,
+                         fbs, gout, gx, gflow, B, C, H, W, tiles_x);
+    else if (agg)
+      hipLaunchKernelGGL((warp_bwd_gx_kernel<BORDER, false, CS, true>), g2, block, 0, s, x, flow,
+                         fbs, gout, gx, gflow, B, C, H, W, tiles_x);
     else
-      hipLaunchKernelGGL((warp_bwd_gx_kernel<BORDER, false, CS>), g2, block, 0, s, x, flow, fbs,
-                         gout, gx, gflow, B, C, H, W, tiles_x);
+      hipLaunchKernelGGL((warp_bwd_gx_kernel<BORDER, false, CS, false>), g2, block, 0, s, x, flow,
+                         fbs, gout, gx, gflow, B, C, H, W, tiles_x);
   } else
     hipLaunchKernelGGL((warp_bwd_kernel<BORDER, false, true, CS>), grid, block, 0, s, x, flow,
                        fbs, gout, gx, gflow, B, C, H, W);
