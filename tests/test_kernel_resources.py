@@ -1,0 +1,37 @@
+"""Register / LDS budgets of the gfx950 kernels (compile-only, no GPU).
+
+The correlation kernels are latency-bound at PWCLite's shapes, so their speed
+rests on occupancy: the default backward tile <d=4, PX=4, SEGX=8, NW=3, CC=4>
+must stay within 168 VGPRs (3 waves/SIMD) and 40 KB of LDS (4 workgroups of
+3 waves per CU), and no kernel may spill to scratch.
+"""
+import shutil
+
+import pytest
+
+from conftest import REPO
+
+pytestmark = pytest.mark.skipif(shutil.which("/opt/rocm/bin/hipcc") is None, reason="hipcc not available")
+
+
+@pytest.fixture(scope="module")
+def corr_resources():
+    import sys
+
+    sys.path.insert(0, str(REPO / "tools"))
+    import kernel_resources
+
+    return kernel_resources.resources(REPO / "unsamflow_amd" / "csrc" / "corr.hip")
+
+
+def test_no_kernel_spills(corr_resources):
+    spilled = [(n, s) for n, _, _, s in corr_resources if s]
+    assert not spilled, spilled
+
+
+def test_default_backward_tile_occupancy(corr_resources):
+    default = [r for r in corr_resources if "corr_bwd_kernelILi4ELi4ELi8ELi3ELi4E" in r[0]]
+    assert default, "default backward instantiation missing"
+    for name, vgpr, lds, _ in default:
+        assert vgpr <= 168, (name, vgpr)
+        assert lds <= 40 * 1024, (name, lds)

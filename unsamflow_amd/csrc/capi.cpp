@@ -28,9 +28,11 @@ static bool check_dims(const char* fn, int B, int C, int H, int W) {
     set_error("%s: non-positive shape B=%d C=%d H=%d W=%d", fn, B, C, H, W);
     return false;
   }
-  // per-sample element offsets are 32-bit inside the kernels
+  // per-sample BYTE offsets are 32-bit inside the kernels (the correlation's
+  // LDS-DMA descriptors span one sample and park masked lanes at 0x7FFFFFF0)
   const long long per_sample = (long long)C * H * W;
-  if (per_sample > INT_MAX || (long long)H * W * 81 > INT_MAX) {
+  const long long max_elems = 0x7FFFFFF0LL / 4 - 1;
+  if (per_sample > max_elems || (long long)H * W * 81 > max_elems) {
     set_error("%s: per-sample tensor too large (C*H*W=%lld)", fn, per_sample);
     return false;
   }

@@ -44,18 +44,82 @@ constexpr int kRsrcFlags = 0x00020000;
 // a byte offset past any plane's num_records (planes are < 2 GiB, checked in capi.cpp)
 constexpr int kOffImage = 0x7FFFFFF0;
 
-using lds_void_t = __attribute__((address_space(3))) void;
+#ifdef USF_TRACE
+// Probe builds only (tools/probes/corr_trace.hip includes this file with
+// USF_TRACE defined): lane 0 of every wave stores s_memrealtime (100 MHz) at
+// phase boundaries, plus its HW_ID/XCC_ID, into g_trace[wave][kTraceSlots].
+constexpr int kTraceSlots = 128;
+__device__ unsigned long long* g_trace;
+__device__ __forceinline__ unsigned trace_wave_id() {
+  return ((blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) * (blockDim.x >> 6) +
+         (threadIdx.x >> 6);
+}
+#define USF_TRACE_AT(slot)                                                                   \
+  do {                                                                                      \
+    if ((threadIdx.x & 63) == 0 && g_trace && (slot) < kTraceSlots - 1)                     \
+      g_trace[(size_t)trace_wave_id() * kTraceSlots + (slot)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#define USF_TRACE_HWID()                                                                     \
+  do {                                                                                      \
+    if ((threadIdx.x & 63) == 0 && g_trace)                                                 \
+      g_trace[(size_t)trace_wave_id() * kTraceSlots + kTraceSlots - 1] =                    \
+          ((unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32) |          \
+          (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);                              \
+  } while (0)
+#define USF_TRACE_VMWAIT() asm volatile("s_waitcnt vmcnt(0)" ::: "memory")
+#else
+#define USF_TRACE_AT(slot) \
+  do {                     \
+  } while (0)
+#define USF_TRACE_HWID() \
+  do {                   \
+  } while (0)
+#define USF_TRACE_VMWAIT() \
+  do {                     \
+  } while (0)
+#endif
 
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t plane_rsrc(const float* plane, bool valid,
-                                                           int plane_bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(plane), (short)0,
-                                           valid ? plane_bytes : 0, kRsrcFlags);
+using lds_void_t = __attribute__((address_space(3))) void;
+using rsrc_t = int __attribute__((ext_vector_type(4)));
+
+// Raw buffer descriptor of one channel plane (stride 0, num_records in bytes;
+// 0 records for a channel past C so its whole stage reads as zeros).
+__device__ __forceinline__ rsrc_t plane_rsrc(const float* plane, bool valid, int plane_bytes) {
+  const uint64_t a = reinterpret_cast<uint64_t>(plane);
+  rsrc_t r;
+  r.x = __builtin_amdgcn_readfirstlane((int)(uint32_t)a);
+  r.y = __builtin_amdgcn_readfirstlane((int)(uint32_t)(a >> 32) & 0xFFFF);
+  r.z = __builtin_amdgcn_readfirstlane(valid ? plane_bytes : 0);
+  r.w = kRsrcFlags;
+  return r;
 }
 
-// One wave-instruction: 64 consecutive floats of LDS at `dst` (wave-uniform)
-// from per-lane byte offsets `voff` of the plane described by `rsrc`.
-__device__ __forceinline__ void dma64(__amdgpu_buffer_rsrc_t rsrc, float* dst, int voff) {
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void_t*)dst, 4, voff, 0, 0, 0);
+// One wave-instruction: 64*V consecutive floats of LDS at `dst` (wave-uniform;
+// lane l fills floats [V*l, V*l+V)) from per-lane byte offsets `voff` of the
+// plane described by `rsrc`. V = 4 is buffer_load_dwordx4 ... lds (1 KiB per
+// instruction, about the issue cost of a 256-B dword DMA).
+// Issued as inline asm on purpose: with the builtin, the compiler cannot tell
+// the in-flight DMA into the other LDS image from the ds_reads of the current
+// one and puts an s_waitcnt vmcnt(0) in front of every ds_read, serialising
+// the prefetch with the FMAs. Completion is awaited explicitly (dma_wait_all +
+// barrier at the end of each stage). M0 holds the LDS destination (an asm
+// input, so the compiler materialises it); the nop is the M0-write -> LDS-DMA
+// hazard wait the compiler emits for the builtin.
+template <int V>
+__device__ __forceinline__ void dma(const rsrc_t& rsrc, float* dst, int voff) {
+  static_assert(V == 1 || V == 4, "dword or dwordx4 LDS-DMA");
+  // low 32 bits of a generic LDS pointer = the LDS byte address (no null check)
+  const int m0 = __builtin_amdgcn_readfirstlane((int)(uint32_t)reinterpret_cast<uintptr_t>(dst));
+  if constexpr (V == 4)
+    asm volatile("s_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds"
+                 :
+                 : "{m0}"(m0), "v"(voff), "s"(rsrc)
+                 : "memory");
+  else
+    asm volatile("s_nop 0\n\tbuffer_load_dword %1, %2, 0 offen lds"
+                 :
+                 : "{m0}"(m0), "v"(voff), "s"(rsrc)
+                 : "memory");
 }
 
 __device__ __forceinline__ void dma_wait_all() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
@@ -125,21 +189,70 @@ __device__ __forceinline__ void lds_read_px8(const float* pa, const float* pw, f
 //    floats (74 at TW=64): each 32-lane group of a b64 read covers all 64
 //    banks once.
 //  * PX == 4: lanes column-major (q = l / TH, r = l % TH), ds_read_b128, row
-//    stride = round_up(TW+2d, 16) + 8 (48 at TW=32).
-// Pad columns of an LDS row are DMA'd as out-of-range zeros.
+//    stride = round_up(TW+2d, 16) (48 at TW=32): conflict-free, where 56 would
+//    cost a 2-way conflict on every window read (tools/lds_banks.py).
+// Pad columns of an LDS row are DMA'd as out-of-range zeros (never read).
+// 16-byte DMA lanes (V = 4) need a row stride that is a multiple of 4 floats
+// and image columns that start 4-aligned: the PX == 4 layout at d == 4 with
+// W % 4 == 0 (every 4-float group is then wholly inside or outside the image).
 template <int PX, int SEGX, int D>
 struct Layout {
   static constexpr int TW = SEGX * PX, TH = 64 / SEGX;
   static constexpr bool B64 = PX == 8;
   static constexpr bool COLMAJOR = PX != 8;
-  static constexpr int S = B64 ? TW + 10 : round_up(TW + 2 * D, 16) + 8;
+  static constexpr int S = B64 ? TW + 10 : round_up(TW + 2 * D, 16);
   static_assert(S >= TW + 2 * D, "row stride must hold the halo row");
+  static constexpr bool X4 = !B64 && S % 4 == 0 && D % 4 == 0;
   __device__ static int row(int lane) { return COLMAJOR ? lane % TH : lane / SEGX; }
   __device__ static int seg(int lane) { return COLMAJOR ? lane / TH : lane % SEGX; }
 };
 
+// One stage of CC channel planes staged HBM -> LDS: plane c of the stage is
+// a ROWS x S image (row stride S, COLS valid columns from global column gx0,
+// rows from gy0) at LDS offset c * PL, PL = ROWS * S rounded up to whole DMA
+// chunks of 64*V floats, filled by CHP chunks per plane spread over NWAVE
+// waves. The per-lane byte offsets are channel- and stage-invariant (one
+// descriptor spans the whole sample; the channel base is added per plane), so
+// each lane keeps only J of them. Lanes outside the image and planes past
+// cend carry kOffImage (hardware zero fill); kOffImage + a channel base stays
+// past num_records (< 2^31, capi.cpp).
+template <int ROWS, int COLS, int S, int CC, int V, int NWAVE>
+struct StageImg {
+  static constexpr int CHUNK = 64 * V;
+  static constexpr int PL = round_up(ROWS * S, CHUNK);  // LDS floats per plane
+  static constexpr int CHP = PL / CHUNK;                // DMA chunks per plane
+  static constexpr int J = (CHP + NWAVE - 1) / NWAVE;   // chunks per wave per plane
+  static constexpr int N = CC * PL;                     // floats per stage image
+  unsigned off[J];
+
+  __device__ __forceinline__ void init(int wave, int lane, int gy0, int gx0, int H, int W) {
+#pragma unroll
+    for (int t = 0; t < J; ++t) {
+      const int e = (wave + t * NWAVE) * CHUNK + lane * V;
+      const int rr = e / S, cc = e - (e / S) * S;
+      const int gy = gy0 + rr, gx = gx0 + cc;
+      const bool ok = rr < ROWS && cc < COLS && (unsigned)gy < (unsigned)H && (unsigned)gx < (unsigned)W;
+      off[t] = ok ? (unsigned)((gy * W + gx) * 4) : (unsigned)kOffImage;
+    }
+  }
+  // channels [c0, c0 + CC) of the sample; channels >= cend read as zeros
+  __device__ __forceinline__ void load(const rsrc_t& rs, float* img, int wave, int c0, int cend,
+                                       int HW) const {
+#pragma unroll
+    for (int c = 0; c < CC; ++c) {
+      const bool cv = c0 + c < cend;
+      const unsigned base = (unsigned)(c0 + c) * (unsigned)HW * 4u;
+#pragma unroll
+      for (int t = 0; t < J; ++t)
+        if (wave + t * NWAVE < CHP)
+          dma<V>(rs, img + c * PL + (wave + t * NWAVE) * CHUNK,
+                 cv ? (int)(off[t] + base) : kOffImage);
+    }
+  }
+};
+
 // ---------------------------------------------------------------- forward --
-template <int D, int PX, int SEGX, int NDY, int CC>
+template <int D, int PX, int SEGX, int NDY, int CC, int V>
 struct FwdCfg {
   static constexpr int K = 2 * D + 1;
   static constexpr int TW = SEGX * PX;              // tile width (pixels)
@@ -150,29 +263,30 @@ struct FwdCfg {
   static constexpr int R2 = TH + NDY - 1;           // staged x2 rows
   static constexpr int C2 = TW + 2 * D;             // staged x2 cols
   static constexpr int S = L::S;                    // LDS row stride (x1 and x2 images)
-  static constexpr int P1 = round_up(TH * S, 64);   // x1 plane image (floats)
-  static constexpr int P2 = round_up(R2 * S, 64);   // x2 plane image
-  static constexpr int CH1 = P1 / 64, CH2 = P2 / 64;  // 64-float chunks per plane
-  static constexpr int J1 = (CH1 + NDY - 1) / NDY;  // chunks per wave per plane
-  static constexpr int J2 = (CH2 + NDY - 1) / NDY;
+  using X1 = StageImg<TH, TW, S, CC, V, NDY>;        // x1 tile, CC planes
+  using X2 = StageImg<R2, C2, S, CC, V, NDY>;        // x2 halo window, CC planes
   static constexpr int WIN = round_up(PX + 2 * D, 4);
-  static constexpr int STAGE = CC * (P1 + P2);
+  static constexpr int STAGE = X1::N + X2::N;
   static constexpr int LDSN = 2 * STAGE + WIN;      // two images + window over-read pad
   static_assert(PX % 4 == 0, "PX must be a multiple of 4 (ds_read_b128)");
   static_assert(64 % SEGX == 0, "SEGX must divide 64");
+  static_assert(V == 1 || L::X4, "16-byte DMA needs the 4-aligned layout");
 };
 
-template <int D, int PX, int SEGX, int NDY, int CC>
+template <int D, int PX, int SEGX, int NDY, int CC, int V>
 __global__ __launch_bounds__(64 * NDY) void corr_fwd_kernel(const float* __restrict__ x1,
                                                             const float* __restrict__ x2,
                                                             float* __restrict__ out, int C,
                                                             int H, int W, int tiles_x) {
-  using F = FwdCfg<D, PX, SEGX, NDY, CC>;
-  constexpr int K = F::K, TW = F::TW, TH = F::TH, C2 = F::C2, S = F::S, P1 = F::P1, P2 = F::P2;
+  using F = FwdCfg<D, PX, SEGX, NDY, CC, V>;
+  constexpr int K = F::K, TW = F::TW, TH = F::TH, S = F::S;
+  constexpr int P1 = F::X1::PL, P2 = F::X2::PL, N1 = F::X1::N;
   constexpr int WIN = F::WIN, STAGE = F::STAGE;
   constexpr bool B64 = F::L::B64;
   __shared__ __attribute__((aligned(16))) float sm[F::LDSN];
 
+  USF_TRACE_AT(0);
+  USF_TRACE_HWID();
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int dyb = blockIdx.x * NDY;
@@ -186,42 +300,16 @@ __global__ __launch_bounds__(64 * NDY) void corr_fwd_kernel(const float* __restr
   const bool active = dy < K;
 
   const int HW = H * W;
-  const float* x1b = x1 + (size_t)b * C * HW;
-  const float* x2b = x2 + (size_t)b * C * HW;
-
-  // stage-invariant per-lane byte offsets of this wave's chunks (row stride S;
-  // pad columns and off-image pixels read as zeros)
-  int vo1[F::J1], vo2[F::J2];
-#pragma unroll
-  for (int t = 0; t < F::J1; ++t) {
-    const int e = (wave + t * NDY) * 64 + lane;
-    const int rr = e / S, cc = e % S;
-    const int gy = y0 + rr, gx = x0 + cc;
-    const bool ok = rr < TH && cc < TW && gy < H && gx < W;
-    vo1[t] = ok ? (gy * W + gx) * 4 : kOffImage;
-  }
-#pragma unroll
-  for (int t = 0; t < F::J2; ++t) {
-    const int e = (wave + t * NDY) * 64 + lane;
-    const int rr = e / S, cc = e % S;
-    const int gy = y0 + dyb - D + rr, gx = x0 - D + cc;
-    const bool ok = rr < F::R2 && cc < C2 && (unsigned)gy < (unsigned)H && (unsigned)gx < (unsigned)W;
-    vo2[t] = ok ? (gy * W + gx) * 4 : kOffImage;
-  }
+  // stage-invariant per-lane DMA offsets (pad columns / off-image pixels: zeros)
+  typename F::X1 s1;
+  typename F::X2 s2;
+  s1.init(wave, lane, y0, x0, H, W);
+  s2.init(wave, lane, y0 + dyb - D, x0 - D, H, W);
+  const rsrc_t r1 = plane_rsrc(x1 + (size_t)b * C * HW, true, C * HW * 4);
+  const rsrc_t r2 = plane_rsrc(x2 + (size_t)b * C * HW, true, C * HW * 4);
   auto dma_stage = [&](int c0, float* img) {
-#pragma unroll
-    for (int c = 0; c < CC; ++c) {
-      const bool cv = c0 + c < C;
-      const auto r1 = plane_rsrc(x1b + (size_t)(c0 + c) * HW, cv, HW * 4);
-      const auto r2 = plane_rsrc(x2b + (size_t)(c0 + c) * HW, cv, HW * 4);
-#pragma unroll
-      for (int t = 0; t < F::J1; ++t)
-        if (wave + t * NDY < F::CH1) dma64(r1, img + c * P1 + (wave + t * NDY) * 64, vo1[t]);
-#pragma unroll
-      for (int t = 0; t < F::J2; ++t)
-        if (wave + t * NDY < F::CH2)
-          dma64(r2, img + CC * P1 + c * P2 + (wave + t * NDY) * 64, vo2[t]);
-    }
+    s1.load(r1, img, wave, c0, C, HW);
+    s2.load(r2, img + N1, wave, c0, C, HW);
   };
 
   float acc[K][PX];
@@ -233,13 +321,15 @@ __global__ __launch_bounds__(64 * NDY) void corr_fwd_kernel(const float* __restr
   dma_stage(0, sm);
   dma_wait_all();
   __syncthreads();
+  USF_TRACE_AT(1);
   int st = 0;
   for (int c0 = 0; c0 < C; c0 += CC, ++st) {
     const float* cur = sm + (st & 1) * STAGE;
     if (c0 + CC < C) dma_stage(c0 + CC, sm + ((st + 1) & 1) * STAGE);  // in flight during FMAs
+    USF_TRACE_AT(2 + 4 * st);
     if (active) {
       const float* p1 = cur + r * S + q * PX;
-      const float* p2 = cur + CC * P1 + (r + wave) * S + q * PX;
+      const float* p2 = cur + N1 + (r + wave) * S + q * PX;
 #pragma unroll 2
       for (int c = 0; c < CC; ++c) {
         float a[PX], w[WIN];
@@ -255,8 +345,11 @@ __global__ __launch_bounds__(64 * NDY) void corr_fwd_kernel(const float* __restr
           for (int i = 0; i < PX; ++i) acc[dx][i] = fmaf(a[i], w[i + dx], acc[dx][i]);
       }
     }
+    USF_TRACE_AT(3 + 4 * st);
     dma_wait_all();
+    USF_TRACE_AT(4 + 4 * st);
     __syncthreads();
+    USF_TRACE_AT(5 + 4 * st);
   }
 
   if (!active) return;
@@ -283,16 +376,26 @@ __global__ __launch_bounds__(64 * NDY) void corr_fwd_kernel(const float* __restr
   }
 }
 
-template <int D, int PX, int SEGX, int NDY, int CC>
-hipError_t launch_fwd(const float* x1, const float* x2, float* out, int B, int C, int H, int W,
-                      hipStream_t s) {
-  using F = FwdCfg<D, PX, SEGX, NDY, CC>;
+template <int D, int PX, int SEGX, int NDY, int CC, int V>
+hipError_t launch_fwd_v(const float* x1, const float* x2, float* out, int B, int C, int H, int W,
+                        hipStream_t s) {
+  using F = FwdCfg<D, PX, SEGX, NDY, CC, V>;
   const int tiles_x = (W + F::TW - 1) / F::TW;
   const int tiles_y = (H + F::TH - 1) / F::TH;
   dim3 grid(F::NDYG, tiles_x * tiles_y, B);
-  hipLaunchKernelGGL((corr_fwd_kernel<D, PX, SEGX, NDY, CC>), grid, dim3(F::NT), 0, s, x1, x2,
-                     out, C, H, W, tiles_x);
+  hipLaunchKernelGGL((corr_fwd_kernel<D, PX, SEGX, NDY, CC, V>), grid, dim3(F::NT), 0, s, x1,
+                     x2, out, C, H, W, tiles_x);
   return hipGetLastError();
+}
+
+// 16-byte DMA staging whenever the layout and W allow it (see Layout).
+template <int D, int PX, int SEGX, int NDY, int CC>
+hipError_t launch_fwd(const float* x1, const float* x2, float* out, int B, int C, int H, int W,
+                      hipStream_t s) {
+  if constexpr (Layout<PX, SEGX, D>::X4) {
+    if (W % 4 == 0) return launch_fwd_v<D, PX, SEGX, NDY, CC, 4>(x1, x2, out, B, C, H, W, s);
+  }
+  return launch_fwd_v<D, PX, SEGX, NDY, CC, 1>(x1, x2, out, B, C, H, W, s);
 }
 
 // Tuning hook: usf_set_variant(0, i) forces candidate i for d=4
@@ -321,18 +424,19 @@ hipError_t fwd_dispatch(const float* x1, const float* x2, float* out, int B, int
     const int forced = variant_override(0);
     if (forced >= 0) return fwd_candidate_d4(forced, x1, x2, out, B, C, H, W, s);
   }
-  // Prefer the big tile (8 px/lane, all displacement rows in one workgroup:
-  // x1/x2 staged once); fall back to smaller tiles / split displacement rows
-  // when that would leave most of the 256 CUs idle.
+  // All displacement rows in one workgroup (x1/x2 staged once) when that
+  // still fills the 256 CUs; else split displacement rows across workgroups.
+  // (profiles/r01_v4_kbench.json: <4,8,9,4> is the fastest d=4 candidate at
+  // the 64x208 level, <4,8,3,8> at 32x104 and below.)
   const long big = (long)B * ((W + 63) / 64) * ((H + 7) / 8);
-  if (big >= 256) return launch_fwd<D, 8, 8, K, 8>(x1, x2, out, B, C, H, W, s);
+  if (big >= 256) return launch_fwd<D, 4, 8, K, 4>(x1, x2, out, B, C, H, W, s);
   const long mid = (long)B * ((W + 31) / 32) * ((H + 7) / 8);
   if (mid >= 256) return launch_fwd<D, 4, 8, K, 8>(x1, x2, out, B, C, H, W, s);
   return launch_fwd<D, 4, 8, 3, 8>(x1, x2, out, B, C, H, W, s);
 }
 
 // --------------------------------------------------------------- backward --
-template <int D, int PX, int SEGX, int NW, int CC>
+template <int D, int PX, int SEGX, int NW, int CC, int V>
 struct BwdCfg {
   static constexpr int K = 2 * D + 1;
   static constexpr int TW = SEGX * PX;
@@ -343,28 +447,29 @@ struct BwdCfg {
   static constexpr int R = TH + 2 * D;               // staged rows
   static constexpr int C2 = TW + 2 * D;              // staged cols
   static constexpr int S = L::S;                     // LDS row stride
-  static constexpr int P = round_up(R * S, 64);      // plane image (floats)
-  static constexpr int CH = P / 64;
-  static constexpr int J = (CH + NW - 1) / NW;       // chunks per wave per plane
+  using X = StageImg<R, C2, S, CC, V, NW>;          // x halo window, CC planes
+  static constexpr int P = X::PL;                    // plane image (floats)
   static constexpr int WIN = round_up(PX + 2 * D, 4);
-  static constexpr int XIMG = CC * P;
+  static constexpr int XIMG = X::N;
   static constexpr int RED = NW * CC * TH * TW;      // per-wave partial sums
-  static constexpr int LDSN = 2 * XIMG + WIN + RED;
+  // <4,4,8,3,4>: 40 KB, so four workgroups fit the 160 KB LDS of a CU
+  static constexpr int LDSN = 2 * XIMG + RED;
   static_assert(PX % 4 == 0, "PX must be a multiple of 4");
+  static_assert(V == 1 || L::X4, "16-byte DMA needs the 4-aligned layout");
 };
 
-// G2 == false: gx1 from (g, x2).  G2 == true: gx2 from (g, x1).
-template <int D, int PX, int SEGX, int NW, int CC, bool G2>
-__global__ __launch_bounds__(64 * NW) void corr_bwd_kernel(const float* __restrict__ xs,
-                                                           const float* __restrict__ g,
-                                                           float* __restrict__ gx, int C, int H,
-                                                           int W, int tiles_x, int cg) {
-  using F = BwdCfg<D, PX, SEGX, NW, CC>;
-  constexpr int K = F::K, TW = F::TW, TH = F::TH, NT = F::NT, C2 = F::C2, S = F::S, P = F::P;
+// One (tile, channel group) of gx1 (G2 == false: from g and x2) or gx2
+// (G2 == true: from g and x1; mirrored indices).
+template <int D, int PX, int SEGX, int NW, int CC, int V, bool G2>
+__device__ __forceinline__ void corr_bwd_tile(float* sm, const float* __restrict__ xs,
+                                              const float* __restrict__ g,
+                                              float* __restrict__ gx, int b, int C, int H, int W,
+                                              int tiles_x, int cg) {
+  using F = BwdCfg<D, PX, SEGX, NW, CC, V>;
+  constexpr int K = F::K, TW = F::TW, TH = F::TH, NT = F::NT, S = F::S, P = F::P;
   constexpr int WIN = F::WIN, DYW = F::DYW, XIMG = F::XIMG;
   constexpr bool B64 = F::L::B64;
-  __shared__ __attribute__((aligned(16))) float sm[F::LDSN];
-  float* red = sm + 2 * XIMG + WIN;
+  float* red = sm + 2 * XIMG;
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -372,7 +477,6 @@ __global__ __launch_bounds__(64 * NW) void corr_bwd_kernel(const float* __restri
   const int tile = blockIdx.x;
   const int cbeg = blockIdx.y * cg;
   const int cend = min(C, cbeg + cg);
-  const int b = blockIdx.z;
   const int ty = tile / tiles_x;
   const int tx = tile - ty * tiles_x;
   const int y0 = ty * TH, x0 = tx * TW;
@@ -402,35 +506,26 @@ __global__ __launch_bounds__(64 * NW) void corr_bwd_kernel(const float* __restri
       }
     }
   }
+  USF_TRACE_VMWAIT();
+  USF_TRACE_AT(1);
 
-  int vo[F::J];
-#pragma unroll
-  for (int t = 0; t < F::J; ++t) {
-    const int e = (wave + t * NW) * 64 + lane;
-    const int rr = e / S, cc = e % S;
-    const int gy = y0 - D + rr, gxx = x0 - D + cc;
-    const bool ok = rr < F::R && cc < C2 && (unsigned)gy < (unsigned)H && (unsigned)gxx < (unsigned)W;
-    vo[t] = ok ? (gy * W + gxx) * 4 : kOffImage;
-  }
-  auto dma_stage = [&](int c0, float* img) {
-#pragma unroll
-    for (int c = 0; c < CC; ++c) {
-      const auto rs = plane_rsrc(xsb + (size_t)(c0 + c) * HW, c0 + c < cend, HW * 4);
-#pragma unroll
-      for (int t = 0; t < F::J; ++t)
-        if (wave + t * NW < F::CH) dma64(rs, img + c * P + (wave + t * NW) * 64, vo[t]);
-    }
-  };
+  typename F::X sx;
+  sx.init(wave, lane, y0 - D, x0 - D, H, W);
+  const rsrc_t rx = plane_rsrc(xsb, true, C * HW * 4);
+  auto dma_stage = [&](int c0, float* img) { sx.load(rx, img, wave, c0, cend, HW); };
 
   const float cf = (float)C;
   float* gxb = gx + (size_t)b * C * HW;
+  const bool vec_out = (W & 3) == 0;
   dma_stage(cbeg, sm);
   dma_wait_all();
   __syncthreads();
+  USF_TRACE_AT(2);
   int st = 0;
   for (int c0 = cbeg; c0 < cend; c0 += CC, ++st) {
     const float* cur = sm + (st & 1) * XIMG;
     if (c0 + CC < cend) dma_stage(c0 + CC, sm + ((st + 1) & 1) * XIMG);
+    USF_TRACE_AT(3 + 4 * st);
     // partials stored lane-linear (lane*PX): conflict-free ds_write_b128
     float* rp = red + wave * (CC * TH * TW) + lane * PX;
 #pragma unroll 2
@@ -458,51 +553,123 @@ __global__ __launch_bounds__(64 * NW) void corr_bwd_kernel(const float* __restri
         reinterpret_cast<float4*>(rp + c * (TH * TW))[i] =
             make_float4(acc[4 * i], acc[4 * i + 1], acc[4 * i + 2], acc[4 * i + 3]);
     }
+    USF_TRACE_AT(4 + 4 * st);
     dma_wait_all();
     __syncthreads();  // partials complete; next stage's image landed
-    for (int o = tid; o < CC * TH * TW; o += NT) {
-      const int c = o / (TH * TW);
-      const int pix = o - c * (TH * TW);
+    USF_TRACE_AT(5 + 4 * st);
+    // combine the NW wave partials in a fixed order, 4 pixels per thread
+    // (a lane's PX pixels are contiguous in its partial slot)
+    for (int o = tid; o < CC * TH * TW / 4; o += NT) {
+      const int c = o / (TH * TW / 4);
+      const int pix = (o - c * (TH * TW / 4)) * 4;
       const int py = pix / TW, pxo = pix % TW;
       // lane that owns pixel (py, pxo) under the layout's lane mapping
       const int ol = F::L::COLMAJOR ? (pxo / PX) * TH + py : py * SEGX + pxo / PX;
       const int ridx = c * (TH * TW) + ol * PX + pxo % PX;
-      float sum = 0.f;
+      float4 sum = *reinterpret_cast<const float4*>(red + ridx);
 #pragma unroll
-      for (int w2 = 0; w2 < NW; ++w2) sum += red[w2 * (CC * TH * TW) + ridx];  // fixed order
+      for (int w2 = 1; w2 < NW; ++w2) {
+        const float4 v = *reinterpret_cast<const float4*>(red + w2 * (CC * TH * TW) + ridx);
+        sum.x += v.x; sum.y += v.y; sum.z += v.z; sum.w += v.w;
+      }
       const int yy = y0 + py, xx = x0 + pxo;
-      if (c0 + c < cend && yy < H && xx < W) gxb[(c0 + c) * HW + yy * W + xx] = sum / cf;
+      if (c0 + c < cend && yy < H) {
+        float* o4 = gxb + (size_t)(c0 + c) * HW + yy * W + xx;
+        if (vec_out && xx + 3 < W) {
+          *reinterpret_cast<float4*>(o4) = make_float4(sum.x / cf, sum.y / cf, sum.z / cf, sum.w / cf);
+        } else {
+          if (xx < W) o4[0] = sum.x / cf;
+          if (xx + 1 < W) o4[1] = sum.y / cf;
+          if (xx + 2 < W) o4[2] = sum.z / cf;
+          if (xx + 3 < W) o4[3] = sum.w / cf;
+        }
+      }
     }
     __syncthreads();  // partial slices free for the next stage
+    USF_TRACE_AT(6 + 4 * st);
   }
 }
 
-template <int D, bool G2, int PX = 4, int SEGX = 8, int NW = 3, int CC = 4>
-hipError_t launch_bwd(const float* xs, const float* g, float* gx, int B, int C, int H, int W,
-                      hipStream_t s) {
-  using F = BwdCfg<D, PX, SEGX, NW, CC>;
+// MODE 1: gx1 only, 2: gx2 only, 3: both (blockIdx.z in [0, 2B): gx1 first).
+// One launch for both directions keeps the whole chip busy through the tail
+// of either half and halves the launch count; the two inlined bodies still
+// fit 3 waves/SIMD at <4,8,3,4> (tools/kernel_resources.py).
+// Budget (tests/test_kernel_resources.py): <4,8,3,4> within 168 VGPRs and
+// 40 KB LDS, i.e. 3 waves/SIMD = 4 resident workgroups of 3 waves per CU.
+template <int D, int PX, int SEGX, int NW, int CC, int V, int MODE>
+__global__ __launch_bounds__(64 * NW) void corr_bwd_kernel(const float* __restrict__ x1,
+                                                           const float* __restrict__ x2,
+                                                           const float* __restrict__ g,
+                                                           float* __restrict__ gx1,
+                                                           float* __restrict__ gx2, int B, int C,
+                                                           int H, int W, int tiles_x, int cg) {
+  __shared__ __attribute__((aligned(16))) float sm[BwdCfg<D, PX, SEGX, NW, CC, V>::LDSN];
+  USF_TRACE_AT(0);
+  USF_TRACE_HWID();
+  int b = blockIdx.z;
+  if constexpr (MODE == 1) {
+    corr_bwd_tile<D, PX, SEGX, NW, CC, V, false>(sm, x2, g, gx1, b, C, H, W, tiles_x, cg);
+  } else if constexpr (MODE == 2) {
+    corr_bwd_tile<D, PX, SEGX, NW, CC, V, true>(sm, x1, g, gx2, b, C, H, W, tiles_x, cg);
+  } else {
+    if (b >= B)
+      corr_bwd_tile<D, PX, SEGX, NW, CC, V, true>(sm, x1, g, gx2, b - B, C, H, W, tiles_x, cg);
+    else
+      corr_bwd_tile<D, PX, SEGX, NW, CC, V, false>(sm, x2, g, gx1, b, C, H, W, tiles_x, cg);
+  }
+}
+
+// Workgroups a backward launch aims for (both directions together): enough to
+// fill the 256 CUs at 3-4 resident workgroups each, and no more -- every
+// extra channel group re-reads its tile's slice of g (81 planes).
+constexpr int kBwdTargetWorkgroups = 768;
+
+template <int D, int PX, int SEGX, int NW, int CC, int V, int MODE>
+hipError_t launch_bwd_mode(const float* x1, const float* x2, const float* g, float* gx1,
+                           float* gx2, int B, int C, int H, int W, hipStream_t s) {
+  using F = BwdCfg<D, PX, SEGX, NW, CC, V>;
+  const int dirs = MODE == 3 ? 2 : 1;
   const int tiles_x = (W + F::TW - 1) / F::TW;
   const int tiles_y = (H + F::TH - 1) / F::TH;
-  const long tiles = (long)tiles_x * tiles_y * B;
-  // channel group per workgroup: g is re-read once per group, so use as few
-  // groups as still give ~512 workgroups
-  int groups = (int)((512 + tiles - 1) / tiles);
+  const long units = (long)tiles_x * tiles_y * B * dirs;
+  int groups = (int)((kBwdTargetWorkgroups + units - 1) / units);
   groups = max(1, min(groups, (C + CC - 1) / CC));
   const int cg = round_up((C + groups - 1) / groups, CC);
-  dim3 grid(tiles_x * tiles_y, (C + cg - 1) / cg, B);
-  hipLaunchKernelGGL((corr_bwd_kernel<D, PX, SEGX, NW, CC, G2>), grid, dim3(F::NT), 0, s, xs, g,
-                     gx, C, H, W, tiles_x, cg);
+  dim3 grid(tiles_x * tiles_y, (C + cg - 1) / cg, B * dirs);
+  hipLaunchKernelGGL((corr_bwd_kernel<D, PX, SEGX, NW, CC, V, MODE>), grid, dim3(F::NT), 0, s, x1,
+                     x2, g, gx1, gx2, B, C, H, W, tiles_x, cg);
   return hipGetLastError();
 }
 
-template <bool G2>
-hipError_t bwd_candidate_d4(int i, const float* xs, const float* g, float* gx, int B, int C, int H,
-                            int W, hipStream_t s) {
+template <int D, int PX, int SEGX, int NW, int CC, int V>
+hipError_t launch_bwd_v(const float* x1, const float* x2, const float* g, float* gx1, float* gx2,
+                        int B, int C, int H, int W, hipStream_t s) {
+  if (gx1 && gx2)
+    return launch_bwd_mode<D, PX, SEGX, NW, CC, V, 3>(x1, x2, g, gx1, gx2, B, C, H, W, s);
+  hipError_t e = hipSuccess;
+  if (gx1) e = launch_bwd_mode<D, PX, SEGX, NW, CC, V, 1>(x1, x2, g, gx1, gx2, B, C, H, W, s);
+  if (e == hipSuccess && gx2)
+    e = launch_bwd_mode<D, PX, SEGX, NW, CC, V, 2>(x1, x2, g, gx1, gx2, B, C, H, W, s);
+  return e;
+}
+
+template <int D, int PX = 4, int SEGX = 8, int NW = 3, int CC = 4>
+hipError_t launch_bwd(const float* x1, const float* x2, const float* g, float* gx1, float* gx2,
+                      int B, int C, int H, int W, hipStream_t s) {
+  if constexpr (Layout<PX, SEGX, D>::X4) {
+    if (W % 4 == 0)
+      return launch_bwd_v<D, PX, SEGX, NW, CC, 4>(x1, x2, g, gx1, gx2, B, C, H, W, s);
+  }
+  return launch_bwd_v<D, PX, SEGX, NW, CC, 1>(x1, x2, g, gx1, gx2, B, C, H, W, s);
+}
+
+hipError_t bwd_candidate_d4(int i, const float* x1, const float* x2, const float* g, float* gx1,
+                            float* gx2, int B, int C, int H, int W, hipStream_t s) {
   switch (i) {
-    case 0: return launch_bwd<4, G2, 4, 8, 3, 4>(xs, g, gx, B, C, H, W, s);
-    case 1: return launch_bwd<4, G2, 4, 8, 3, 8>(xs, g, gx, B, C, H, W, s);
-    case 2: return launch_bwd<4, G2, 4, 8, 9, 4>(xs, g, gx, B, C, H, W, s);
-    case 3: return launch_bwd<4, G2, 4, 8, 9, 8>(xs, g, gx, B, C, H, W, s);
+    case 0: return launch_bwd<4, 4, 8, 3, 4>(x1, x2, g, gx1, gx2, B, C, H, W, s);
+    case 1: return launch_bwd<4, 4, 8, 3, 8>(x1, x2, g, gx1, gx2, B, C, H, W, s);
+    case 2: return launch_bwd<4, 4, 8, 9, 4>(x1, x2, g, gx1, gx2, B, C, H, W, s);
+    case 3: return launch_bwd<4, 4, 8, 9, 8>(x1, x2, g, gx1, gx2, B, C, H, W, s);
     default: return hipErrorInvalidValue;
   }
 }
@@ -511,18 +678,11 @@ constexpr int kBwdCandidates = 4;
 template <int D>
 hipError_t bwd_dispatch(const float* x1, const float* x2, const float* g, float* gx1, float* gx2,
                         int B, int C, int H, int W, hipStream_t s) {
-  hipError_t e = hipSuccess;
   if (D == 4) {
     const int forced = variant_override(1);
-    if (forced >= 0) {
-      if (gx1) e = bwd_candidate_d4<false>(forced, x2, g, gx1, B, C, H, W, s);
-      if (e == hipSuccess && gx2) e = bwd_candidate_d4<true>(forced, x1, g, gx2, B, C, H, W, s);
-      return e;
-    }
+    if (forced >= 0) return bwd_candidate_d4(forced, x1, x2, g, gx1, gx2, B, C, H, W, s);
   }
-  if (gx1) e = launch_bwd<D, false>(x2, g, gx1, B, C, H, W, s);
-  if (e == hipSuccess && gx2) e = launch_bwd<D, true>(x1, g, gx2, B, C, H, W, s);
-  return e;
+  return launch_bwd<D>(x1, x2, g, gx1, gx2, B, C, H, W, s);
 }
 
 }  // namespace

@@ -142,21 +142,42 @@ __global__ __launch_bounds__(256) void warp_bwd_kernel(const float* __restrict__
     const int y = p / W, xx = p - y * W;
     const float* fb = flow + b * fbs;
     tp = make_tap(fb[p], fb[HW + p], xx, y, H, W, BORDER);
+  } else {
+    tp.m_nw = tp.m_ne = tp.m_sw = tp.m_se = false;
+  }
+  // grad_x atomics: consecutive lanes are consecutive pixels, so lane l's
+  // east corners usually hit the same cells as lane l+1's west corners.
+  // Such pairs are merged through a lane shuffle: the right lane adds the left
+  // lane's east contribution into its own west atomic and the left lane skips
+  // its east atomic (~2 instead of 4 global atomics per pixel and channel).
+  bool take_n = false, take_s = false, give_n = false, give_s = false;
+  if (WANT_GX) {
+    const int left_ne = __shfl_up(tp.m_ne ? tp.o_ne : -1, 1);
+    const int left_se = __shfl_up(tp.m_se ? tp.o_se : -1, 1);
+    const bool has_left = pl > 0 && (t & 63) != 0;
+    take_n = has_left && tp.m_nw && left_ne == tp.o_nw;
+    take_s = has_left && tp.m_sw && left_se == tp.o_sw;
+    give_n = __shfl_down(take_n ? 1 : 0, 1) != 0 && pl + 1 < PXB && (t & 63) != 63;
+    give_s = __shfl_down(take_s ? 1 : 0, 1) != 0 && pl + 1 < PXB && (t & 63) != 63;
+  }
+  {
     const float wnw = tp.s * tp.e, wne = tp.s * tp.w, wsw = tp.n * tp.e, wse = tp.n * tp.w;
     const float* xb = x + (size_t)b * C * HW;
-    const float* gb = gout + (size_t)b * C * HW + p;
+    const float* gb = gout + (size_t)b * C * HW + (valid ? p : 0);
     float* gxb = WANT_GX ? gx + (size_t)b * C * HW : nullptr;
 #pragma unroll 4
     for (int c = slice; c < C; c += CS) {
-      const float go = gb[(size_t)c * HW];
+      const float go = valid ? gb[(size_t)c * HW] : 0.f;
       if (WANT_GX) {
+        const float vne = go * wne, vse = go * wse;
+        const float lne = __shfl_up(vne, 1), lse = __shfl_up(vse, 1);
         float* gc = gxb + (size_t)c * HW;
-        if (tp.m_nw) atomicAdd(gc + tp.o_nw, go * wnw);
-        if (tp.m_ne) atomicAdd(gc + tp.o_ne, go * wne);
-        if (tp.m_sw) atomicAdd(gc + tp.o_sw, go * wsw);
-        if (tp.m_se) atomicAdd(gc + tp.o_se, go * wse);
+        if (tp.m_nw) atomicAdd(gc + tp.o_nw, go * wnw + (take_n ? lne : 0.f));
+        if (tp.m_ne && !give_n) atomicAdd(gc + tp.o_ne, vne);
+        if (tp.m_sw) atomicAdd(gc + tp.o_sw, go * wsw + (take_s ? lse : 0.f));
+        if (tp.m_se && !give_s) atomicAdd(gc + tp.o_se, vse);
       }
-      if (WANT_GF) {
+      if (WANT_GF && valid) {
         const float* xc = xb + (size_t)c * HW;
         const float vnw = tp.m_nw ? xc[tp.o_nw] : 0.f;
         const float vne = tp.m_ne ? xc[tp.o_ne] : 0.f;
@@ -375,8 +396,18 @@ void bwd_launch_cs(const float* x, const float* flow, long long fbs, const float
     constexpr int TPX = 256 / CS, TW = TPX >= 16 ? 16 : TPX, TH = TPX / TW;
     const int tiles_x = (W + TW - 1) / TW, tiles_y = (H + TH - 1) / TH;
     const dim3 g2((unsigned)(tiles_x * tiles_y), (unsigned)B);
-    // usf_set_variant(2, v): 0 = LDS-aggregated scatter, 1 = direct global atomics
-    const bool agg = variant_override(2) != 1;
+    // usf_set_variant(2, v): 0 = lane-merged direct atomics (default), 1 = LDS-aggregated tiles
+    const int v = variant_override(2);
+    if (v != 1) {
+      if (gflow)
+        hipLaunchKernelGGL((warp_bwd_kernel<BORDER, true, true, CS>), grid, block, 0, s, x, flow,
+                           fbs, gout, gx, gflow, B, C, H, W);
+      else
+        hipLaunchKernelGGL((warp_bwd_kernel<BORDER, true, false, CS>), grid, block, 0, s, x, flow,
+                           fbs, gout, gx, gflow, B, C, H, W);
+      return;
+    }
+    const bool agg = true;
     if (gflow && agg)
       hipLaunchKernelGGL((warp_bwd_gx_kernel<BORDER, true, CS, true>), g2, block, 0, s, x, flow,
                          fbs, gout, gx, gflow, B, C, H, W, tiles_x);
