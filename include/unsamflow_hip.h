@@ -95,8 +95,9 @@ int usf_warp_bwd_f32(const float* x, const float* flow, long long flow_bstride,
 /* Tuning hook (benchmarking only; not needed for correct use).
  * Forces kernel variant `index` of `op` for d=4 launches in this process:
  * op 0 = correlation forward tile config, op 1 = correlation backward tile
- * config, op 2 = warp grad_x scatter (0 = lane-merged direct global atomics,
- * 1 = LDS-aggregated tiles); index -1 restores the built-in choice. Returns the number of
+ * config, op 2 = warp grad_x scatter (0 = wave reduce-by-key + direct global
+ * atomics, 1 = LDS-aggregated tiles, 2 / 3 = variant 0 with 4 / 1 channel
+ * slices per workgroup); index -1 restores the built-in choice. Returns the number of
  * variants of `op` (so index range is [0, n)), or USF_EINVAL for an unknown op
  * or out-of-range index. Process-wide; set it before launching, not
  * concurrently with launches. */

@@ -338,9 +338,10 @@ def test_corr_every_tile_variant_vs_oracle(hip_device, shape):
         lib.usf_set_variant(1, -1)
 
 
-@pytest.mark.parametrize("variant", [0, 1])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3])
 def test_warp_grad_x_scatter_variants(hip_device, variant):
-    """LDS-aggregated and direct-atomic grad_x scatters both match the oracle,
+    """Every grad_x scatter variant (reduce-by-key atomics with any channel split,
+    LDS-aggregated tiles) matches the oracle,
     including a large-flow case whose target boxes overflow the LDS budget."""
     from unsamflow_amd import _lib, ops
 

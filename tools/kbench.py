@@ -66,7 +66,7 @@ def main():
             res.append(dict(op="warp_fwd", shape=list(k), us=round(us, 2), gbps=round(warp_bytes(B, C, H, W) / us / 1e3, 1)))
             print(res[-1], flush=True)
             k = (B, C, H, W, "border", True, True)
-            for v in (-1, 0, 1):
+            for v in (-1, 0, 1, 2, 3):
                 lib.usf_set_variant(2, v)
                 us = device_time_us(site_launcher("warp_bwd", k, dev))
                 res.append(dict(op="warp_bwd", shape=list(k), variant=v, us=round(us, 2),

@@ -119,6 +119,71 @@ __global__ __launch_bounds__(256) void warp_fwd_kernel(const float* __restrict__
   }
 }
 
+// grad_x scatter of one corner row (north: nw/ne, or south: sw/se) as a
+// wave-level reduce-by-key. Consecutive lanes are consecutive pixels, so along
+// a wave the target cells of a row are (nearly) monotone: lanes whose west
+// corner hits the same cell (the flow compresses, or floor() of a coordinate
+// that round-trips a hair below an integer) form a RUN, and a run's east cell
+// is usually the next run's west cell. Each run is summed onto its last lane
+// (log-step segmented scan over shuffles; the bound is the longest run in the
+// wave, channel-invariant, so the common no-collision case costs 2 shuffles),
+// the next run's head adds the previous run's east total into its west value,
+// and only run tails issue atomics: ~1 global atomic per cell and channel, and
+// no two lanes of one atomic instruction on the same address (those serialise).
+struct RowRuns {
+  int pos;      // lane's distance from its run head
+  int maxlen;   // longest run in the wave (wave-uniform)
+  bool tail;    // last lane of its run: issues the run's atomics
+  bool take;    // run head that adds the previous run's east total (cells chain)
+  bool give;    // run tail whose east total the next run's head takes
+};
+
+// key: row * (W + 1) + west column + 1, or a lane-unique negative value when the
+// row is outside the image (no atomics); has_left/has_right: the neighbour lane
+// exists and belongs to the same channel slice.
+__device__ __forceinline__ RowRuns row_runs(int key, bool m_w, bool m_e, bool has_left,
+                                            bool has_right) {
+  const int lane = threadIdx.x & 63;
+  const int kl = __shfl_up(key, 1);
+  const bool left_me = __shfl_up(m_e ? 1 : 0, 1) != 0;
+  const bool head = !(has_left && kl == key);
+  const unsigned long long heads = __ballot(head);
+  const unsigned long long upto = lane == 63 ? ~0ull : ((2ull << lane) - 1);
+  RowRuns r;
+  r.pos = lane - (63 - __clzll(heads & upto));
+  r.tail = lane == 63 || ((heads >> (lane + 1)) & 1ull) != 0;
+  int m = r.pos;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = max(m, __shfl_xor(m, o));
+  r.maxlen = m + 1;
+  r.take = head && has_left && m_w && left_me && kl + 1 == key;
+  // every cross-lane read executes in all lanes (never behind a short-circuit:
+  // a ds_bpermute from an inactive lane returns garbage)
+  const bool right_takes = __shfl_down(r.take ? 1 : 0, 1) != 0;
+  r.give = r.tail && has_right && right_takes;
+  return r;
+}
+
+// segmented inclusive scan: lane l ends with the sum over [its run head, l]
+__device__ __forceinline__ float run_sum(float v, const RowRuns& r) {
+  for (int d = 1; d < r.maxlen; d <<= 1) {
+    const float u = __shfl_up(v, d);
+    if (r.pos >= d) v += u;
+  }
+  return v;
+}
+
+__device__ __forceinline__ void scatter_row(float* gc, int o_w, int o_e, bool m_w, bool m_e,
+                                            float vw, float ve, const RowRuns& r) {
+  const float se = run_sum(ve, r);
+  const float lt = __shfl_up(se, 1);
+  const float sw = run_sum(vw + (r.take ? lt : 0.f), r);
+  if (r.tail) {
+    if (m_w) atomicAdd(gc + o_w, sw);
+    if (m_e && !r.give) atomicAdd(gc + o_e, se);
+  }
+}
+
 template <bool BORDER, bool WANT_GX, bool WANT_GF, int CS>
 __global__ __launch_bounds__(256) void warp_bwd_kernel(const float* __restrict__ x,
                                                        const float* __restrict__ flow,
@@ -145,37 +210,34 @@ __global__ __launch_bounds__(256) void warp_bwd_kernel(const float* __restrict__
   } else {
     tp.m_nw = tp.m_ne = tp.m_sw = tp.m_se = false;
   }
-  // grad_x atomics: consecutive lanes are consecutive pixels, so lane l's
-  // east corners usually hit the same cells as lane l+1's west corners.
-  // Such pairs are merged through a lane shuffle: the right lane adds the left
-  // lane's east contribution into its own west atomic and the left lane skips
-  // its east atomic (~2 instead of 4 global atomics per pixel and channel).
-  bool take_n = false, take_s = false, give_n = false, give_s = false;
+  // grad_x: reduce-by-key over the wave per corner row (see scatter_row)
+  RowRuns rn{}, rs{};
   if (WANT_GX) {
-    const int left_ne = __shfl_up(tp.m_ne ? tp.o_ne : -1, 1);
-    const int left_se = __shfl_up(tp.m_se ? tp.o_se : -1, 1);
-    const bool has_left = pl > 0 && (t & 63) != 0;
-    take_n = has_left && tp.m_nw && left_ne == tp.o_nw;
-    take_s = has_left && tp.m_sw && left_se == tp.o_sw;
-    give_n = __shfl_down(take_n ? 1 : 0, 1) != 0 && pl + 1 < PXB && (t & 63) != 63;
-    give_s = __shfl_down(take_s ? 1 : 0, 1) != 0 && pl + 1 < PXB && (t & 63) != 63;
+    const int lane = t & 63;
+    const bool has_left = pl > 0 && lane != 0;
+    const bool has_right = pl + 1 < PXB && lane != 63;
+    // keys alias nothing only for west columns in [-1, W-1] (zeros padding can
+    // put xw anywhere; outside that range both corners of the row are off-image)
+    const bool vx = tp.xw >= -1 && tp.xw < W;
+    const bool vyn = valid && vx && (unsigned)tp.yn < (unsigned)H;
+    const bool vys = valid && vx && (unsigned)(tp.yn + 1) < (unsigned)H;
+    const int kn = vyn ? tp.yn * (W + 1) + tp.xw + 1 : -(lane + 2);
+    const int ks = vys ? (tp.yn + 1) * (W + 1) + tp.xw + 1 : -(lane + 2);
+    rn = row_runs(kn, tp.m_nw, tp.m_ne, has_left, has_right);
+    rs = row_runs(ks, tp.m_sw, tp.m_se, has_left, has_right);
   }
   {
     const float wnw = tp.s * tp.e, wne = tp.s * tp.w, wsw = tp.n * tp.e, wse = tp.n * tp.w;
     const float* xb = x + (size_t)b * C * HW;
     const float* gb = gout + (size_t)b * C * HW + (valid ? p : 0);
     float* gxb = WANT_GX ? gx + (size_t)b * C * HW : nullptr;
-#pragma unroll 4
+#pragma unroll 2
     for (int c = slice; c < C; c += CS) {
       const float go = valid ? gb[(size_t)c * HW] : 0.f;
       if (WANT_GX) {
-        const float vne = go * wne, vse = go * wse;
-        const float lne = __shfl_up(vne, 1), lse = __shfl_up(vse, 1);
         float* gc = gxb + (size_t)c * HW;
-        if (tp.m_nw) atomicAdd(gc + tp.o_nw, go * wnw + (take_n ? lne : 0.f));
-        if (tp.m_ne && !give_n) atomicAdd(gc + tp.o_ne, vne);
-        if (tp.m_sw) atomicAdd(gc + tp.o_sw, go * wsw + (take_s ? lse : 0.f));
-        if (tp.m_se && !give_s) atomicAdd(gc + tp.o_se, vse);
+        scatter_row(gc, tp.o_nw, tp.o_ne, tp.m_nw, tp.m_ne, go * wnw, go * wne, rn);
+        scatter_row(gc, tp.o_sw, tp.o_se, tp.m_sw, tp.m_se, go * wsw, go * wse, rs);
       }
       if (WANT_GF && valid) {
         const float* xc = xb + (size_t)c * HW;
@@ -396,7 +458,7 @@ void bwd_launch_cs(const float* x, const float* flow, long long fbs, const float
     constexpr int TPX = 256 / CS, TW = TPX >= 16 ? 16 : TPX, TH = TPX / TW;
     const int tiles_x = (W + TW - 1) / TW, tiles_y = (H + TH - 1) / TH;
     const dim3 g2((unsigned)(tiles_x * tiles_y), (unsigned)B);
-    // usf_set_variant(2, v): 0 = lane-merged direct atomics (default), 1 = LDS-aggregated tiles
+    // usf_set_variant(2, v): 1 = LDS-aggregated tiles; otherwise lane-merged direct atomics
     const int v = variant_override(2);
     if (v != 1) {
       if (gflow)
@@ -428,7 +490,17 @@ void bwd_launch_cs(const float* x, const float* flow, long long fbs, const float
 template <bool BORDER>
 void bwd_launch_pad(const float* x, const float* flow, long long fbs, const float* gout,
                     float* gx, float* gflow, int B, int C, int H, int W, hipStream_t s) {
-  switch (pick_cs(B, C, H * W)) {
+  // usf_set_variant(2, 2 / 3): lane-merged scatter with CS forced to 4 / 1
+  // (whole-wave pixel runs) instead of the occupancy-driven choice
+  const int v = variant_override(2);
+  // Default: CS = 4 (each wave one 64-pixel run of one channel, so an atomic
+  // wave-instruction covers one contiguous row piece) whenever that still gives
+  // ~100 workgroups; narrower pixel runs (CS 16/64) only for the tiny levels.
+  // tools/wbench.py: L3 48 vs 61 us, L2 35 vs 57 us (CS 4 vs 16); L1 (8x26,
+  // 32 workgroups at CS 4) 26 us at CS 64 vs 44 us.
+  const long runs64 = (long)B * ((H * W + 63) / 64);
+  const int cs = v == 2 ? 4 : v == 3 ? 1 : (runs64 >= 96 && C >= 4) ? 4 : pick_cs(B, C, H * W);
+  switch (cs) {
     case 1: bwd_launch_cs<BORDER, 1>(x, flow, fbs, gout, gx, gflow, B, C, H, W, s); break;
     case 4: bwd_launch_cs<BORDER, 4>(x, flow, fbs, gout, gx, gflow, B, C, H, W, s); break;
     case 16: bwd_launch_cs<BORDER, 16>(x, flow, fbs, gout, gx, gflow, B, C, H, W, s); break;
