@@ -16,7 +16,13 @@ Output: ONE JSON line on rank 0 with the driver's contract fields plus
 * ``levels`` — per call site (op, level shape) mean us, GB/s, HBM fraction;
 * ``cpu_baseline`` — the oracle's torch-CPU restatement of the same step
   (correlation_native-style correlation + grid_sample warp) on the host cores,
-  rank 0 at N=1 only, bounded sample.
+  rank 0 at N=1 only, bounded sample; plus SURVEY.md §8d's config-1 / config-2
+  correlation fwd/bwd times on the CPU oracle;
+* ``survey_configs`` — the same two correlation configs on the GPU kernels;
+* ``roofline.copy_ceiling_gbps`` — a measured device-copy (STREAM-copy) rate
+  on this box, and ``roofline.traffic`` — HBM bytes per launch of the roofline
+  kernel from the committed rocprofv3 PMC passes (profiles/*_pmc_traffic.json,
+  tools/pmc_traffic.py) when they cover that kernel and shape.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
                        [--config kitti|sintel_mf] [--no-cpu-baseline]
@@ -32,6 +38,8 @@ import time
 REPO = os.path.dirname(os.path.abspath(__file__))
 if REPO not in sys.path:
     sys.path.insert(0, REPO)
+
+import glob  # noqa: E402
 
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
@@ -103,6 +111,72 @@ def kernel_report(summary, device, steps):
     return rows, roof, {k: round(v, 1) for k, v in per_op.items()}
 
 
+SURVEY_CONFIGS = {"cfg1": (2, 32, 64, 128), "cfg2": (8, 128, 32, 104)}
+
+
+def copy_ceiling_gbps(device, mib=512, reps=10):
+    """Measured device-to-device copy rate (read + write bytes / time)."""
+    a = torch.empty(mib * 1024 * 1024 // 4, device=device)
+    b = torch.empty_like(a)
+    b.copy_(a)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        b.copy_(a)
+    e1.record()
+    e1.synchronize()
+    sec = e0.elapsed_time(e1) / 1e3 / reps
+    del a, b
+    return round(2 * mib * 1024 * 1024 / sec / 1e9, 1)
+
+
+def pmc_traffic(op, shape):
+    """HBM bytes per launch of (op, shape) from the newest committed PMC summary."""
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_traffic.json")))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        data = json.load(f)
+    for site in data.get("sites", []):
+        if site["op"] == op and list(site["shape"]) == list(shape):
+            return site["traffic_bytes"], os.path.relpath(files[-1], REPO)
+    return None, None
+
+
+def survey_configs_gpu(device):
+    from unsamflow_amd.kernel_timer import device_time_us, site_launcher
+
+    out = {}
+    for name, (B, C, H, W) in SURVEY_CONFIGS.items():
+        f = device_time_us(site_launcher("corr_fwd", (B, C, H, W), device))
+        b = device_time_us(site_launcher("corr_bwd", (B, C, H, W, True, True), device))
+        out[name] = {"shape": [B, C, H, W], "fwd_us": round(f, 2), "bwd_us": round(b, 2)}
+    return out
+
+
+def survey_configs_cpu():
+    """SURVEY §8d configs on the CPU oracle (correlation_native restatement, autograd bwd)."""
+    from oracle.corr import OracleCorrelation
+
+    corr = OracleCorrelation(4)
+    out = {}
+    for name, (B, C, H, W) in SURVEY_CONFIGS.items():
+        g = torch.Generator().manual_seed(0)
+        x1 = torch.randn(B, C, H, W, generator=g, requires_grad=True)
+        x2 = torch.randn(B, C, H, W, generator=g, requires_grad=True)
+        go = torch.randn(B, 81, H, W, generator=g)
+        corr(x1, x2).backward(go)  # warm both directions
+        x1.grad = x2.grad = None
+        t0 = time.perf_counter()
+        y = corr(x1, x2)
+        t1 = time.perf_counter()
+        y.backward(go)
+        t2 = time.perf_counter()
+        out[name] = {"shape": [B, C, H, W], "fwd_ms": round((t1 - t0) * 1e3, 2),
+                     "bwd_ms": round((t2 - t1) * 1e3, 2)}
+    return out
+
+
 def cpu_baseline(args, cfg_name):
     """Oracle (torch-CPU restatement) PWCLite step on the host cores, bounded."""
     from oracle.torch_ref import OracleCorrelation, oracle_flow_warp
@@ -129,8 +203,10 @@ def cpu_baseline(args, cfg_name):
             model = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), "")
     except OSError:
         pass
+    configs = survey_configs_cpu()
     return {
         "value": round(args.cpu_batch * args.cpu_steps / dt, 4),
+        "survey_configs": configs,
         "unit": "image-pairs/s",
         "cores": cores,
         "kind": "port",
@@ -192,6 +268,12 @@ def main():
     torch.cuda.synchronize()
     summary = kt.summary()
     rows, roof, per_op_us = kernel_report(summary, device, args.profile_steps)
+    roof["copy_ceiling_gbps"] = copy_ceiling_gbps(device)
+    roof["frac_of_copy"] = round(roof["achieved"] / roof["copy_ceiling_gbps"], 4)
+    traffic, src = pmc_traffic(roof["kernel"], roof["shape"])
+    roof["traffic"] = traffic
+    roof["traffic_source"] = src
+    gpu_configs = survey_configs_gpu(device)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -225,6 +307,7 @@ def main():
             "roofline": roof,
             "cpu_baseline": cpu,
             "hot_path_device_us_per_step": per_op_us,
+            "survey_configs": gpu_configs,
             "levels": rows,
             "final_loss": round(loss_val, 6),
         }

@@ -1,0 +1,33 @@
+"""Build A/B variants of libunsamflow_hip.so with compile-time knobs, for
+side-by-side timing on the GPU box (load one with USF_LIB=<path>).
+
+Usage: python tools/ab_build.py name:-DFLAG=V,-DFLAG2=V ...  -> unsamflow_amd/lib/ab/lib_<name>.so
+"""
+import subprocess
+import sys
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parent.parent
+CSRC = REPO / "unsamflow_amd" / "csrc"
+OUT = REPO / "unsamflow_amd" / "lib" / "ab"
+FLAGS = ["-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950"]
+
+
+def build(name, defines):
+    OUT.mkdir(parents=True, exist_ok=True)
+    objs = []
+    for src in ("corr.hip", "warp.hip", "capi.cpp"):
+        obj = OUT / f"{name}_{Path(src).stem}.o"
+        lang = ["-x", "hip"] if src.endswith(".hip") else []
+        subprocess.run(["/opt/rocm/bin/hipcc", *FLAGS, *defines, *lang, "-c", str(CSRC / src), "-o", str(obj)],
+                       check=True)
+        objs.append(str(obj))
+    so = OUT / f"lib_{name}.so"
+    subprocess.run(["/opt/rocm/bin/hipcc", "-shared", "--offload-arch=gfx950", "-o", str(so), *objs], check=True)
+    print(so)
+
+
+if __name__ == "__main__":
+    for arg in sys.argv[1:]:
+        name, _, defs = arg.partition(":")
+        build(name, [d for d in defs.split(",") if d])

@@ -11,13 +11,12 @@ import torch  # noqa: E402
 from unsamflow_amd import _lib  # noqa: E402
 from unsamflow_amd.kernel_timer import site_launcher  # noqa: E402
 
-SITES = [
-    ("corr_fwd", (8, 32, 64, 208)), ("corr_bwd", (8, 32, 64, 208, True, True)),
-    ("corr_fwd", (8, 64, 32, 104)), ("corr_bwd", (8, 64, 32, 104, True, True)),
-    ("corr_fwd", (8, 192, 4, 13)), ("corr_bwd", (8, 192, 4, 13, True, True)),
-    ("warp_bwd", (8, 32, 64, 208, "border", True, True)), ("warp_fwd", (8, 32, 64, 208, "border")),
-    ("warp_bwd", (8, 3, 256, 832, "border", False, True)),
-]
+KITTI = [(192, 4, 13), (128, 8, 26), (96, 16, 52), (64, 32, 104), (32, 64, 208)]
+SITES = [("corr_fwd", (8, C, H, W)) for C, H, W in KITTI]
+SITES += [("corr_bwd", (8, C, H, W, True, True)) for C, H, W in KITTI]
+SITES += [("warp_fwd", (8, C, H, W, "border")) for C, H, W in KITTI[1:]]
+SITES += [("warp_bwd", (8, C, H, W, "border", True, True)) for C, H, W in KITTI[1:]]
+SITES += [("warp_fwd", (8, 3, 256, 832, "border")), ("warp_bwd", (8, 3, 256, 832, "border", False, True))]
 
 
 def main():

@@ -1,0 +1,80 @@
+"""HBM traffic per launch of each hot-path call site from rocprofv3 PMC passes.
+
+Input: the FETCH_SIZE and WRITE_SIZE passes of tools/gpu_pmc.sh over
+tools/kprof.py (each its own rocprofv3 --pmc run with --kernel-trace only).
+kprof.py launches, in order: a 256 MiB device copy (n times, calibration),
+then every site of kprof.SITES n times; each site launch contains exactly one
+usf:: kernel, so usf dispatches map to sites by order.
+
+Correction (MI355X_MICROARCH.md, HBM/rocprofv3): FETCH_SIZE under-reports
+wide streaming reads by 2x on gfx950 and other access widths are uncalibrated,
+so both counters are scaled by the factor that makes the calibration copy
+read / write exactly its 268,435,456 bytes. Output: JSON with, per site,
+fetch/write KiB (median over launches), corrected traffic bytes per launch and
+the algorithmic bytes for comparison.
+
+Usage: python tools/pmc_traffic.py gpurun_out/pmc > profiles/rNN_pmc_traffic.json
+"""
+import csv
+import json
+import os
+import statistics
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+COPY_BYTES = 64 * 1024 * 1024 * 4
+
+
+def per_dispatch(path, counter):
+    rows = list(csv.DictReader(open(path)))
+    d = {}
+    for r in rows:
+        if r["Counter_Name"] != counter:
+            continue
+        did = int(r["Dispatch_Id"])
+        d.setdefault(did, [r["Kernel_Name"], 0.0])
+        d[did][1] += float(r["Counter_Value"])
+    return [d[k] for k in sorted(d)]
+
+
+def main():
+    root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc"
+    from kprof import SITES
+    from unsamflow_amd.kernel_timer import corr_bytes, warp_bytes
+
+    n = int(os.environ.get("KPROF_N", "3"))
+    fetch = per_dispatch(f"{root}/p3/run_counter_collection.csv", "FETCH_SIZE")
+    write = per_dispatch(f"{root}/p4/run_counter_collection.csv", "WRITE_SIZE")
+
+    def calib(rows):
+        copies = [v for name, v in rows if "copy" in name.lower()][:n]
+        return COPY_BYTES / (statistics.median(copies) * 1024)
+
+    f_read, f_write = calib(fetch), calib(write)
+    uf = [v for name, v in fetch if "usf::" in name]
+    uw = [v for name, v in write if "usf::" in name]
+    sites = []
+    for i, (op, key) in enumerate(SITES):
+        fk = statistics.median(uf[i * n:(i + 1) * n])
+        wk = statistics.median(uw[i * n:(i + 1) * n])
+        if op.startswith("corr"):
+            alg = corr_bytes(*key[:4], backward=op == "corr_bwd")
+        elif op == "warp_fwd":
+            alg = warp_bytes(*key[:4])
+        else:
+            alg = warp_bytes(*key[:4], True, key[5], key[6])
+        traffic = fk * 1024 * f_read + wk * 1024 * f_write
+        sites.append({"op": op, "shape": list(key), "fetch_kib": round(fk, 1), "write_kib": round(wk, 1),
+                      "traffic_bytes": int(traffic), "algorithmic_bytes": int(alg),
+                      "traffic_over_algorithmic": round(traffic / alg, 3)})
+    print(json.dumps({"calibration": {"copy_bytes": COPY_BYTES, "fetch_scale": round(f_read, 4),
+                                      "write_scale": round(f_write, 4), "launches_per_site": n},
+                      "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes, --kernel-trace only) "
+                                "over tools/kprof.py, scaled by a 256 MiB copy calibration",
+                      "sites": sites}, indent=1))
+
+
+if __name__ == "__main__":
+    main()

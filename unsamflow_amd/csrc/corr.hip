@@ -207,6 +207,27 @@ struct Layout {
   __device__ static int seg(int lane) { return COLMAJOR ? lane / TH : lane % SEGX; }
 };
 
+// Workgroups are dealt round-robin over the 8 XCDs, so blocks b and b + 8 share
+// an L2 (MI355X_MICROARCH.md §Workgroup dispatch; a speed property, never a
+// correctness one). Renumber the linear block id so that CONSECUTIVE work items
+// -- which share staged data (a tile's displacement-row groups / channel
+// groups, neighbouring tiles' halos) -- run on one XCD. Bijective on [0, n).
+// Used by the forward kernel (L3 16.7 vs 18.6 us, FETCH traffic 3.9x -> 1.0x of
+// algorithmic). USF_XCD_REMAP=0 (tools/ab_build.py A/B builds) turns it off.
+#ifndef USF_XCD_REMAP
+#define USF_XCD_REMAP 1
+#endif
+__device__ __forceinline__ int xcd_remap(int lin, int n) {
+  if (!USF_XCD_REMAP) return lin;
+  const int full = n & ~7;
+  if (lin >= full) return lin;
+  return (lin & 7) * (full >> 3) + (lin >> 3);
+}
+
+__device__ __forceinline__ int linear_block() {
+  return blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+}
+
 // One stage of CC channel planes staged HBM -> LDS: plane c of the stage is
 // a ROWS x S image (row stride S, COLS valid columns from global column gx0,
 // rows from gy0) at LDS offset c * PL, PL = ROWS * S rounded up to whole DMA
@@ -289,9 +310,11 @@ __global__ __launch_bounds__(64 * NDY) void corr_fwd_kernel(const float* __restr
   USF_TRACE_HWID();
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int dyb = blockIdx.x * NDY;
-  const int tile = blockIdx.y;
-  const int b = blockIdx.z;
+  // work item: displacement-row group fastest, then tile, then sample
+  const int w = xcd_remap(linear_block(), gridDim.x * gridDim.y * gridDim.z);
+  const int dyb = (w % F::NDYG) * NDY;
+  const int tile = (w / F::NDYG) % gridDim.y;
+  const int b = w / (F::NDYG * gridDim.y);
   const int ty = tile / tiles_x;
   const int tx = tile - ty * tiles_x;
   const int y0 = ty * TH, x0 = tx * TW;
@@ -463,8 +486,8 @@ struct BwdCfg {
 template <int D, int PX, int SEGX, int NW, int CC, int V, bool G2>
 __device__ __forceinline__ void corr_bwd_tile(float* sm, const float* __restrict__ xs,
                                               const float* __restrict__ g,
-                                              float* __restrict__ gx, int b, int C, int H, int W,
-                                              int tiles_x, int cg) {
+                                              float* __restrict__ gx, int tile, int group, int b,
+                                              int C, int H, int W, int tiles_x, int cg) {
   using F = BwdCfg<D, PX, SEGX, NW, CC, V>;
   constexpr int K = F::K, TW = F::TW, TH = F::TH, NT = F::NT, S = F::S, P = F::P;
   constexpr int WIN = F::WIN, DYW = F::DYW, XIMG = F::XIMG;
@@ -474,8 +497,7 @@ __device__ __forceinline__ void corr_bwd_tile(float* sm, const float* __restrict
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int tile = blockIdx.x;
-  const int cbeg = blockIdx.y * cg;
+  const int cbeg = group * cg;
   const int cend = min(C, cbeg + cg);
   const int ty = tile / tiles_x;
   const int tx = tile - ty * tiles_x;
@@ -596,8 +618,13 @@ __device__ __forceinline__ void corr_bwd_tile(float* sm, const float* __restrict
 // fit 3 waves/SIMD at <4,8,3,4> (tools/kernel_resources.py).
 // Budget (tests/test_kernel_resources.py): <4,8,3,4> within 168 VGPRs and
 // 40 KB LDS, i.e. 3 waves/SIMD = 4 resident workgroups of 3 waves per CU.
+// amdgpu_waves_per_eu(3) pins the VGPR target: without it, allocation for the
+// two inlined direction bodies flips between 163 and 231 on unrelated edits.
 template <int D, int PX, int SEGX, int NW, int CC, int V, int MODE>
-__global__ __launch_bounds__(64 * NW) void corr_bwd_kernel(const float* __restrict__ x1,
+#ifndef USF_BWD_WAVES_PER_EU
+#define USF_BWD_WAVES_PER_EU 3
+#endif
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(USF_BWD_WAVES_PER_EU))) void corr_bwd_kernel(const float* __restrict__ x1,
                                                            const float* __restrict__ x2,
                                                            const float* __restrict__ g,
                                                            float* __restrict__ gx1,
@@ -606,16 +633,25 @@ __global__ __launch_bounds__(64 * NW) void corr_bwd_kernel(const float* __restri
   __shared__ __attribute__((aligned(16))) float sm[BwdCfg<D, PX, SEGX, NW, CC, V>::LDSN];
   USF_TRACE_AT(0);
   USF_TRACE_HWID();
-  int b = blockIdx.z;
+  // work item: channel group fastest (the groups of a tile share its g planes),
+  // then tile, then (direction, sample); grid = (tiles, groups, B * dirs).
+  // No XCD remap here: tools/ab_build.py A/B on the box, L4 59 us without vs
+  // 85 us with it (FETCH traffic 2.6x -> 1.4x of algorithmic, yet slower).
+  const int w = linear_block();
+  const int group = w % gridDim.y;
+  const int tile = (w / gridDim.y) % gridDim.x;
+  int b = w / (gridDim.x * gridDim.y);
   if constexpr (MODE == 1) {
-    corr_bwd_tile<D, PX, SEGX, NW, CC, V, false>(sm, x2, g, gx1, b, C, H, W, tiles_x, cg);
+    corr_bwd_tile<D, PX, SEGX, NW, CC, V, false>(sm, x2, g, gx1, tile, group, b, C, H, W, tiles_x, cg);
   } else if constexpr (MODE == 2) {
-    corr_bwd_tile<D, PX, SEGX, NW, CC, V, true>(sm, x1, g, gx2, b, C, H, W, tiles_x, cg);
+    corr_bwd_tile<D, PX, SEGX, NW, CC, V, true>(sm, x1, g, gx2, tile, group, b, C, H, W, tiles_x, cg);
   } else {
     if (b >= B)
-      corr_bwd_tile<D, PX, SEGX, NW, CC, V, true>(sm, x1, g, gx2, b - B, C, H, W, tiles_x, cg);
+      corr_bwd_tile<D, PX, SEGX, NW, CC, V, true>(sm, x1, g, gx2, tile, group, b - B, C, H, W,
+                                                  tiles_x, cg);
     else
-      corr_bwd_tile<D, PX, SEGX, NW, CC, V, false>(sm, x2, g, gx1, b, C, H, W, tiles_x, cg);
+      corr_bwd_tile<D, PX, SEGX, NW, CC, V, false>(sm, x2, g, gx1, tile, group, b, C, H, W,
+                                                   tiles_x, cg);
   }
 }
 
