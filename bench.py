@@ -9,11 +9,16 @@ random-init weights. N>1: one process per GPU (torchrun), DDP over RCCL
 ("nccl"), B=8 per rank (weak scaling).
 
 Output: ONE JSON line on rank 0 with the driver's contract fields plus
-* ``roofline`` — the dominant hot-path kernel (largest summed time per step):
-  algorithmic bytes per launch / its mean duration, measured
-  with HIP events on the launch stream in an instrumented pass of real steps
-  that follows the timed region;
-* ``levels`` — per call site (op, level shape) mean us, GB/s, HBM fraction;
+* ``roofline`` — the dominant hot-path call site (largest summed time per
+  step): algorithmic bytes per launch / its mean launch
+  duration, measured with HIP events on the launch stream around every
+  library launch INSIDE the timed region (unsamflow_amd.kernel_timer); with
+  USF_ROCTX=1 each launch is also a roctx range, so ``rocprofv3 --kernel-trace
+  --stats --kernel-rename --marker-trace`` lists the same site as one row
+  (tools/roofline_check.py compares the two);
+* ``levels`` — per call site (op, level shape): in-step mean us (timed
+  region) and device us of graph-replayed launches on synthetic inputs of
+  that shape, GB/s, HBM fraction;
 * ``cpu_baseline`` — the oracle's torch-CPU restatement of the same step
   (correlation_native-style correlation + grid_sample warp) on the host cores,
   rank 0 at N=1 only, bounded sample; plus SURVEY.md §8d's config-1 / config-2
@@ -61,7 +66,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=6)
     ap.add_argument("--cpu-batch", type=int, default=4)
-    ap.add_argument("--profile-steps", type=int, default=3, help="instrumented steps for per-kernel timing")
+    ap.add_argument("--no-replay", action="store_true",
+                    help="skip the graph-replay device times (keeps a rocprofv3 run to real steps only)")
     ap.add_argument("--cudnn-benchmark", action="store_true",
                     help="MIOpen find-mode tuning of the convolutions (slow first steps)")
     return ap.parse_args()
@@ -73,40 +79,46 @@ def cfg_for(name):
     return kitti_base() if name == "kitti" else sintel_mf()
 
 
-def kernel_report(summary, device, steps):
-    """Per call site: in-step (event-bracketed) time, device time (graph replay),
-    algorithmic GB/s and HBM fraction; plus the dominant kernel's roofline."""
-    from unsamflow_amd.kernel_timer import device_time_us, site_launcher
+def kernel_report(summary, device, steps, replay=True):
+    """Per call site: in-step time (events around each launch in the timed
+    region), device time of graph-replayed launches, algorithmic GB/s and HBM
+    fraction; plus the roofline of the dominant site (by in-step time)."""
+    from unsamflow_amd.kernel_timer import device_time_us, site_launcher, site_name
 
     rows, per_op = [], {}
     best = None
     for i, ((op, key), a) in enumerate(summary.items()):
-        dev_us = device_time_us(site_launcher(op, key, device, seed=i))
         calls = a["n"] / max(1, steps)
-        gbps = a["bytes"] / (dev_us * 1e-6) / 1e9
+        us = a["mean_us"]
         row = {
-            "op": op, "shape": list(key), "calls_per_step": calls, "device_us": round(dev_us, 2),
-            "in_step_us": round(a["mean_us"], 2), "bytes": a["bytes"], "gbps": round(gbps, 1),
-            "hbm_frac": round(gbps / HBM_PEAK_GBPS, 4),
-            "tflops": round(a["flops"] / (dev_us * 1e-6) / 1e12, 2),
+            "op": op, "shape": list(key), "site": site_name(op, key), "calls_per_step": calls,
+            "in_step_us": round(us, 2), "bytes": a["bytes"], "gbps": round(a["bytes"] / (us * 1e-6) / 1e9, 1),
+            "hbm_frac": round(a["bytes"] / (us * 1e-6) / 1e9 / HBM_PEAK_GBPS, 4),
+            "tflops": round(a["flops"] / (us * 1e-6) / 1e12, 2),
         }
+        if replay:
+            row["device_us"] = round(device_time_us(site_launcher(op, key, device, seed=i)), 2)
         rows.append(row)
-        per_op[op] = per_op.get(op, 0.0) + calls * dev_us
-        if best is None or calls * dev_us > best[0]:
-            best = (calls * dev_us, row)
+        per_op[op] = per_op.get(op, 0.0) + calls * us
+        if best is None or calls * us > best[0]:
+            best = (calls * us, row)
     row = best[1]
     roof = {
         "bound": "hbm",
         "kernel": row["op"],
         "shape": row["shape"],
+        "site": row["site"],
         "achieved": row["gbps"],
         "peak": HBM_PEAK_GBPS,
         "unit": "GB/s",
         "frac": row["hbm_frac"],
         "bytes_per_launch": row["bytes"],
-        "mean_us": row["device_us"],
+        "mean_us": row["in_step_us"],
+        "launches_timed": int(round(row["calls_per_step"] * steps)),
+        "replay_us": row.get("device_us"),
         "traffic": None,
-        "method": "algorithmic bytes (SURVEY 8d) / device time of 20 graph-replayed launches (HIP events)",
+        "method": "algorithmic bytes (SURVEY 8d) / mean duration of the site's launches in the timed region "
+                  "(HIP events on the launch stream)",
     }
     return rows, roof, {k: round(v, 1) for k, v in per_op.items()}
 
@@ -248,10 +260,11 @@ def main():
     if distributed:
         dist.barrier()
     torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        loss = step(img1, img2, s1, s2)
-    torch.cuda.synchronize()
+    with KernelTimer() as kt:  # two event records per hot-path launch, no syncs
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            loss = step(img1, img2, s1, s2)
+        torch.cuda.synchronize()
     if distributed:
         dist.barrier()
     elapsed = time.perf_counter() - t0
@@ -261,19 +274,14 @@ def main():
         elapsed = t.item()
     loss_val = float(loss.item())
 
-    # instrumented pass: per-launch HIP events around every hot-path kernel
-    with KernelTimer() as kt:
-        for _ in range(args.profile_steps):
-            step(img1, img2, s1, s2)
-    torch.cuda.synchronize()
     summary = kt.summary()
-    rows, roof, per_op_us = kernel_report(summary, device, args.profile_steps)
+    rows, roof, per_op_us = kernel_report(summary, device, args.steps, replay=not args.no_replay)
     roof["copy_ceiling_gbps"] = copy_ceiling_gbps(device)
     roof["frac_of_copy"] = round(roof["achieved"] / roof["copy_ceiling_gbps"], 4)
     traffic, src = pmc_traffic(roof["kernel"], roof["shape"])
     roof["traffic"] = traffic
     roof["traffic_source"] = src
-    gpu_configs = survey_configs_gpu(device)
+    gpu_configs = None if args.no_replay else survey_configs_gpu(device)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -306,7 +314,7 @@ def main():
             },
             "roofline": roof,
             "cpu_baseline": cpu,
-            "hot_path_device_us_per_step": per_op_us,
+            "hot_path_us_per_step": per_op_us,
             "survey_configs": gpu_configs,
             "levels": rows,
             "final_loss": round(loss_val, 6),

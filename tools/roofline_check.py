@@ -1,0 +1,38 @@
+"""Cross-check bench.py's roofline timing against rocprofv3.
+
+Reads the JSON line of a bench.py run made under
+``USF_ROCTX=1 rocprofv3 --kernel-trace --stats --kernel-rename --marker-trace``
+and that run's kernel_stats.csv, where every hot-path launch is listed under
+its call-site name (unsamflow_amd.kernel_timer.site_name). Prints, for the
+roofline site and every other hot-path site, the bench's in-step event mean
+next to rocprof's average duration (rocprof also counts the warm-up steps).
+
+Usage: python tools/roofline_check.py bench_prof.json run_kernel_stats.csv
+"""
+import csv
+import json
+import sys
+
+
+def main():
+    bench = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
+    stats = {r["Name"]: r for r in csv.DictReader(open(sys.argv[2]))}
+    roof = bench["roofline"]
+    sites = []
+    for row in bench["levels"]:
+        st = stats.get(row["site"])
+        entry = {"site": row["site"], "bench_in_step_us": row["in_step_us"],
+                 "rocprof_avg_us": round(float(st["AverageNs"]) / 1e3, 2) if st else None,
+                 "rocprof_calls": int(st["Calls"]) if st else None}
+        if st:
+            entry["rel_diff"] = round(entry["rocprof_avg_us"] / row["in_step_us"] - 1, 4)
+        sites.append(entry)
+    top = next(e for e in sites if e["site"] == roof["site"])
+    print(json.dumps({"roofline_site": roof["site"], "roofline_mean_us": roof["mean_us"],
+                      "rocprof_avg_us": top["rocprof_avg_us"], "rel_diff": top.get("rel_diff"),
+                      "sites": sites}, indent=1))
+    return 0 if top["rocprof_avg_us"] is not None else 1
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -8,10 +8,14 @@ on (torch's current stream — the stream ops.py hands to the library):
   training step and its call site (op, shape, flags) is recorded. These
   in-step intervals include any time the GPU waits for the host to enqueue
   the kernel, so they bound the kernel time from above.
-* ``device_time_us`` — the kernel's device time: REPS launches of one call
-  site captured into a HIP graph, replayed back to back between two events,
-  divided by the launch count. No host gaps; this is what ``roofline`` uses and
-  what ``rocprofv3 --kernel-trace --stats`` reports as the average duration.
+* ``device_time_us`` — the kernel's device time on synthetic inputs of the
+  call site's shape: REPS launches captured into a HIP graph, replayed back to
+  back between two events, divided by the launch count (no host gaps).
+
+With ``USF_ROCTX=1`` every launch through :mod:`unsamflow_amd.ops` is also
+wrapped in a roctx range named after its call site (``site_name``), so
+``rocprofv3 --kernel-trace --stats --kernel-rename --marker-trace`` reports
+one row per call site, comparable with the in-step means (tools/roofline_check.py).
 
 Algorithmic bytes / flops per launch follow SURVEY.md §8(d): every input read
 once, every output written once (halo re-reads, scratch and zero-fill
@@ -21,10 +25,34 @@ from __future__ import annotations
 
 import collections
 import contextlib
+import ctypes
+import os
 
 import torch
 
 _active: "KernelTimer | None" = None
+_roctx = None
+
+
+def site_name(op: str, key) -> str:
+    """Stable call-site label, e.g. ``usf:warp_bwd:8x32x64x208:border:1:1``."""
+    return "usf:" + op + ":" + "x".join(str(k) for k in key[:4]) + "".join(f":{k}" for k in key[4:])
+
+
+def _roctx_lib():
+    global _roctx
+    if _roctx is None:
+        _roctx = False
+        if os.environ.get("USF_ROCTX") == "1":
+            for name in ("librocprofiler-sdk-roctx.so.1", "librocprofiler-sdk-roctx.so", "libroctx64.so"):
+                try:
+                    lib = ctypes.CDLL(name)
+                    lib.roctxRangePushA.argtypes = [ctypes.c_char_p]
+                    _roctx = lib
+                    break
+                except OSError:
+                    continue
+    return _roctx
 
 
 def corr_bytes(B, C, H, W, K2=81, backward=False, need1=True, need2=True):
@@ -82,21 +110,28 @@ class KernelTimer:
 @contextlib.contextmanager
 def timed(op: str, key, device, nbytes: int, flops: int = 0):
     """Bracket one launch (used by ops.py)."""
-    kt = _active
-    if kt is None:
+    rx = _roctx_lib()
+    if rx:
+        rx.roctxRangePushA(site_name(op, key).encode())
+    try:
+        kt = _active
+        if kt is None:
+            yield
+            return
+        if not kt.time_in_step:
+            yield
+            kt.records.append((op, key, None, None, nbytes, flops))
+            return
+        s = torch.cuda.Event(enable_timing=True)
+        e = torch.cuda.Event(enable_timing=True)
+        stream = torch.cuda.current_stream(device)
+        s.record(stream)
         yield
-        return
-    if not kt.time_in_step:
-        yield
-        kt.records.append((op, key, None, None, nbytes, flops))
-        return
-    s = torch.cuda.Event(enable_timing=True)
-    e = torch.cuda.Event(enable_timing=True)
-    stream = torch.cuda.current_stream(device)
-    s.record(stream)
-    yield
-    e.record(stream)
-    kt.records.append((op, key, s, e, nbytes, flops))
+        e.record(stream)
+        kt.records.append((op, key, s, e, nbytes, flops))
+    finally:
+        if rx:
+            rx.roctxRangePop()
 
 
 def site_launcher(op: str, key, device, seed: int = 0):
