@@ -191,7 +191,7 @@ def survey_configs_cpu():
 
 def cpu_baseline(args, cfg_name):
     """Oracle (torch-CPU restatement) PWCLite step on the host cores, bounded."""
-    from oracle.torch_ref import OracleCorrelation, oracle_flow_warp
+    from oracle.torch_ref import OracleCorrelation, oracle_flow_warp, oracle_occu_mask_backward
     from unsamflow_amd.harness import TrainStep, synthetic_pair
 
     try:
@@ -202,7 +202,7 @@ def cpu_baseline(args, cfg_name):
     torch.set_num_threads(cores)
     c = CONFIGS[cfg_name]
     step = TrainStep(cfg_for(cfg_name), "cpu", corr_module=OracleCorrelation(4), warp_fn=oracle_flow_warp,
-                     fused_adam=False)
+                     occ_backward_fn=oracle_occu_mask_backward, fused_adam=False)
     img1, img2, s1, s2 = synthetic_pair(args.cpu_batch, c["H"], c["W"], "cpu", with_seg=cfg_name != "kitti")
     step(img1, img2, s1, s2)  # warmup
     t0 = time.perf_counter()
@@ -223,7 +223,7 @@ def cpu_baseline(args, cfg_name):
         "cores": cores,
         "kind": "port",
         "sample": f"{args.cpu_steps} steps x B={args.cpu_batch} ({c['W']}x{c['H']}) of the same train step on CPU "
-                  f"with the oracle restatement (oracle/torch_ref.py) for corr+warp, after 1 warmup step; "
+                  f"with the oracle restatement (oracle/torch_ref.py) for corr+warp+occlusion, after 1 warmup step; "
                   f"{dt:.1f} s; {model}",
     }
 

@@ -17,6 +17,10 @@
  *                        mesh_grid :7-13 and norm_grid :16-23)
  *   usf_warp_bwd_f32  <- grid_sampler_2d_backward reached from flow_warp's
  *                        autograd graph (warp_utils.py:103-105)
+ *   usf_splat_map_f32 <- get_corresponding_map (warp_utils.py:26-94,
+ *                        scatter_add_ of bilinear weights)
+ *   usf_occ_backward_f32 <- get_occu_mask_backward (warp_utils.py:120-126),
+ *                        caller losses/flow_loss.py:101-103 (occ_from_back)
  *
  * Contract (all entry points):
  *   - Pointers are DEVICE pointers to fp32 NCHW tensors. x/x1/x2/gout/out/gx*
@@ -91,6 +95,22 @@ int usf_warp_fwd_f32(const float* x, const float* flow, long long flow_bstride,
 int usf_warp_bwd_f32(const float* x, const float* flow, long long flow_bstride,
                      const float* gout, float* gx, float* gflow,
                      int B, int C, int H, int W, int pad_mode, void* stream);
+
+/* Forward bilinear splat of unit mass (get_corresponding_map,
+ * utils/warp_utils.py:26-94): every source pixel p lands at
+ *   (x, y) = absolute ? (flow[b,0,p], flow[b,1,p]) : (px + flow[b,0,p], py + flow[b,1,p])
+ * and adds (1-|x-cx|)*(1-|y-cy|) to each of its 4 integer neighbours inside
+ * the image. map: [B,1,H,W] dense, overwritten (zeroed by the call on the
+ * stream, then accumulated with fp32 atomics: summation order not fixed).
+ * flow: [B,2,H,W] with batch stride flow_bstride. */
+int usf_splat_map_f32(const float* flow, long long flow_bstride, float* map,
+                      int B, int H, int W, int absolute, void* stream);
+
+/* Occlusion mask from the backward flow (get_occu_mask_backward,
+ * warp_utils.py:120-126): occ = clamp(splat_map(flow21), 0, 1) < th ? 1 : 0.
+ * occ: [B,1,H,W] dense, overwritten. */
+int usf_occ_backward_f32(const float* flow21, long long flow_bstride, float* occ,
+                         int B, int H, int W, float th, void* stream);
 
 /* Tuning hook (benchmarking only; not needed for correct use).
  * Forces kernel variant `index` of `op` for d=4 launches in this process:

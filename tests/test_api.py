@@ -78,10 +78,10 @@ def test_mesh_and_norm_grid_semantics():
     assert n[0, 0, 0].tolist() == [-1.0, -1.0] and n[0, 2, 3].tolist() == [1.0, 1.0]
 
 
-def test_occlusion_mask_backward_zero_flow_is_visible():
-    flow = torch.zeros(1, 2, 5, 6)
-    occ = warp_utils.get_occu_mask_backward(flow)
-    assert occ.shape == (1, 1, 5, 6) and occ.sum() == 0
-    # a flow pushing everything out of the image occludes everything
-    occ2 = warp_utils.get_occu_mask_backward(torch.full((1, 2, 5, 6), 100.0))
-    assert occ2.sum() == 30
+def test_occlusion_entry_points_have_no_cpu_path():
+    """get_occu_mask_backward / get_corresponding_map run the HIP splat kernel only."""
+    with pytest.raises(RuntimeError, match="no CPU path"):
+        warp_utils.get_occu_mask_backward(torch.zeros(1, 2, 5, 6))
+    with pytest.raises(RuntimeError, match="no CPU path"):
+        warp_utils.get_corresponding_map(torch.zeros(1, 2, 5, 6))
+

@@ -27,12 +27,13 @@ def _worker(rank, world, port, out_dir):
     torch.set_num_threads(2)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from oracle.hashrng import hash_init_
-    from oracle.torch_ref import OracleCorrelation, oracle_flow_warp
+    from oracle.torch_ref import OracleCorrelation, oracle_flow_warp, oracle_occu_mask_backward
     from unsamflow_amd.config import kitti_base
     from unsamflow_amd.harness import TrainStep, synthetic_pair
 
     cfg = kitti_base()
-    step = TrainStep(cfg, "cpu", ddp=True, corr_module=OracleCorrelation(4), warp_fn=oracle_flow_warp)
+    step = TrainStep(cfg, "cpu", ddp=True, corr_module=OracleCorrelation(4), warp_fn=oracle_flow_warp,
+                     occ_backward_fn=oracle_occu_mask_backward)
     hash_init_(step.module, seed=3)
     # DDP broadcast happened at construction; re-sync after the deterministic init
     for p in step.module.parameters():

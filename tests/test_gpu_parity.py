@@ -358,3 +358,59 @@ def test_warp_grad_x_scatter_variants(hip_device, variant):
             np.testing.assert_allclose(_np(gf), rf, atol=1e-4, rtol=1e-5)
     finally:
         lib.usf_set_variant(2, -1)
+
+
+# ---------------------------------------------------------------- occlusion --
+def _occ_flow_dev(z, dev):
+    f = torch.from_numpy(z["flow_full"]).to(dev)
+    return f[:, 2:] if int(z["slice"]) else f
+
+
+def _assert_occ_equal(occ, ref, cmap_ref, th=0.2, eps=1e-5):
+    """Masks equal except where the reference map sits within eps of the threshold
+    (fp32 atomics sum in a different order than scatter_add_)."""
+    bad = occ != ref
+    assert not np.any(bad & (np.abs(np.clip(cmap_ref, 0, 1) - th) > eps)), int(bad.sum())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", golden_files("occ_"))
+def test_occlusion_vs_reference_golden(hip_device, name):
+    """usf_splat_map_f32 / usf_occ_backward_f32 vs the reference's
+    get_corresponding_map / get_occu_mask_backward captures."""
+    from unsamflow_amd import warp_utils
+
+    z = load_golden(name)
+    flow = _occ_flow_dev(z, hip_device)
+    B, _, H, W = flow.shape
+    ys, xs = torch.meshgrid(torch.arange(H, device=hip_device), torch.arange(W, device=hip_device), indexing="ij")
+    coords = torch.stack([xs, ys], 0).float().expand(B, 2, H, W) + flow
+    cmap = warp_utils.get_corresponding_map(coords)
+    np.testing.assert_allclose(_np(cmap), z["map"], atol=2e-6, rtol=1e-6)
+    occ = warp_utils.get_occu_mask_backward(flow, th=0.2)
+    _assert_occ_equal(_np(occ), z["occ"], z["map"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape,scale", [((8, 256, 832), 4.0), ((8, 256, 832), 0.0), ((2, 64, 208), 30.0),
+                                         ((3, 33, 17), 2.5)])
+def test_occlusion_vs_oracle_full_size(hip_device, shape, scale):
+    """The loss's call site ([B,2,256,832] backward flow, B=8) and odd shapes vs the
+    oracle; relative-displacement form vs absolute-coordinate form."""
+    from oracle.torch_ref import oracle_corresponding_map, oracle_occu_mask_backward
+    from unsamflow_amd import ops
+
+    B, H, W = shape
+    flow = torch.from_numpy(hashrng.symmetric((B, 2, H, W), 9100 + H, scale)) if scale else torch.zeros(B, 2, H, W)
+    occ = ops.occ_backward(flow.to(hip_device), 0.2)
+    ref = oracle_occu_mask_backward(flow, 0.2)
+    ys, xs = torch.meshgrid(torch.arange(H), torch.arange(W), indexing="ij")
+    coords = torch.stack([xs, ys], 0).float().expand(B, 2, H, W) + flow
+    cmap_ref = oracle_corresponding_map(coords).numpy()
+    _assert_occ_equal(_np(occ), ref.numpy(), cmap_ref)
+    rel = _np(ops.splat_map(flow.to(hip_device)))
+    absm = _np(ops.splat_map(coords.to(hip_device), absolute=True))
+    np.testing.assert_allclose(rel, cmap_ref, atol=2e-6, rtol=1e-6)
+    np.testing.assert_allclose(absm, cmap_ref, atol=2e-6, rtol=1e-6)
+    # mass conservation: every in-image target spreads exactly its weights
+    assert abs(float(rel.sum()) - float(cmap_ref.sum())) < 1e-3 * max(1.0, float(cmap_ref.sum()))

@@ -7,7 +7,7 @@ import torch
 
 from conftest import load_golden
 from oracle.hashrng import hash_init_
-from oracle.torch_ref import OracleCorrelation, oracle_flow_warp
+from oracle.torch_ref import OracleCorrelation, oracle_flow_warp, oracle_occu_mask_backward
 from unsamflow_amd.config import AttrDict, kitti_base, sintel_mf
 from unsamflow_amd.flow_loss import unFlowLoss
 from unsamflow_amd.pwclite import PWCLite
@@ -17,7 +17,8 @@ def _run(name, cfg):
     z = load_golden(f"pwclite_{name}.npz")
     model = PWCLite(AttrDict.wrap(dict(cfg.model)), corr_module=OracleCorrelation(4), warp_fn=oracle_flow_warp)
     hash_init_(model, seed=1)
-    loss_fn = unFlowLoss(AttrDict.wrap(dict(cfg.loss)), warp_fn=oracle_flow_warp)
+    loss_fn = unFlowLoss(AttrDict.wrap(dict(cfg.loss)), warp_fn=oracle_flow_warp,
+                         occ_backward_fn=oracle_occu_mask_backward)
     img1, img2 = torch.from_numpy(z["img1"]), torch.from_numpy(z["img2"])
     kw = {}
     if "seg1" in z:
@@ -58,7 +59,8 @@ def test_train_step_runs_on_cpu_with_oracle_ops():
     from unsamflow_amd.harness import TrainStep, synthetic_pair
 
     cfg = kitti_base()
-    step = TrainStep(cfg, "cpu", corr_module=OracleCorrelation(4), warp_fn=oracle_flow_warp)
+    step = TrainStep(cfg, "cpu", corr_module=OracleCorrelation(4), warp_fn=oracle_flow_warp,
+                     occ_backward_fn=oracle_occu_mask_backward)
     img1, img2, _, _ = synthetic_pair(1, 64, 128, "cpu")
     before = [p.detach().clone() for p in step.module.parameters()]
     loss = step(img1, img2)
@@ -71,7 +73,7 @@ def test_homography_smoothness_is_rejected():
     cfg = kitti_base()
     cfg.loss.w_sm = 0.1
     cfg.loss.smooth_type = "homography"
-    loss_fn = unFlowLoss(cfg.loss, warp_fn=oracle_flow_warp)
+    loss_fn = unFlowLoss(cfg.loss, warp_fn=oracle_flow_warp, occ_backward_fn=oracle_occu_mask_backward)
     flows = [torch.zeros(1, 4, 64 >> i, 128 >> i) for i in range(5)]
     with pytest.raises(NotImplementedError):
         loss_fn(flows, torch.rand(1, 3, 64, 128), torch.rand(1, 3, 64, 128))

@@ -99,3 +99,32 @@ def test_hashrng_is_stable():
         hashrng.uniform((3,), 1), np.array([0.7663017511367798, 0.12603098154067993, 0.700931191444397], np.float32)
     )
     np.testing.assert_allclose(hashrng.normal((2,), 3), [0.023737091571092606, -0.9943225979804993], rtol=1e-6)
+
+
+def _occ_flow(z):
+    f = torch.from_numpy(z["flow_full"])
+    return f[:, 2:] if int(z["slice"]) else f
+
+
+@pytest.mark.parametrize("name", golden_files("occ_"))
+def test_occlusion_oracle_matches_reference(name):
+    """oracle_corresponding_map / oracle_occu_mask_backward == the reference's
+    get_corresponding_map / get_occu_mask_backward (warp_utils.py:26-94, 120-126)."""
+    from oracle.torch_ref import oracle_corresponding_map, oracle_occu_mask_backward
+
+    z = load_golden(name)
+    flow = _occ_flow(z)
+    B, _, H, W = flow.shape
+    xs = torch.arange(W, dtype=torch.float32).view(1, 1, W).expand(B, H, W)
+    ys = torch.arange(H, dtype=torch.float32).view(1, H, 1).expand(B, H, W)
+    cmap = oracle_corresponding_map(torch.stack([xs, ys], 1) + flow)
+    np.testing.assert_allclose(cmap.numpy(), z["map"], atol=1e-6, rtol=0)
+    np.testing.assert_array_equal(oracle_occu_mask_backward(flow, th=0.2).numpy(), z["occ"])
+
+
+def test_occlusion_oracle_zero_and_outward_flow():
+    from oracle.torch_ref import oracle_occu_mask_backward
+
+    assert oracle_occu_mask_backward(torch.zeros(1, 2, 5, 6)).sum() == 0
+    # a flow pushing everything out of the image occludes everything
+    assert oracle_occu_mask_backward(torch.full((1, 2, 5, 6), 100.0)).sum() == 30

@@ -44,6 +44,14 @@ _SIGNATURES = {
         + [ctypes.c_void_p],
         ctypes.c_int,
     ),
+    "usf_splat_map_f32": (
+        [_c_float_p, ctypes.c_longlong, _c_float_p] + [ctypes.c_int] * 4 + [ctypes.c_void_p],
+        ctypes.c_int,
+    ),
+    "usf_occ_backward_f32": (
+        [_c_float_p, ctypes.c_longlong, _c_float_p] + [ctypes.c_int] * 3 + [ctypes.c_float, ctypes.c_void_p],
+        ctypes.c_int,
+    ),
     "usf_set_variant": ([ctypes.c_int, ctypes.c_int], ctypes.c_int),
 }
 EXPORTED_SYMBOLS = tuple(_SIGNATURES)

@@ -165,6 +165,40 @@ int usf_warp_bwd_f32(const float* x, const float* flow, long long flow_bstride,
                 (hipStream_t)stream);
 }
 
+static bool check_splat(const char* fn, const float* flow, long long fbs, const float* out, int B,
+                        int H, int W) {
+  if (!check_dims(fn, B, 2, H, W)) return false;
+  if (!flow || !out) {
+    set_error("%s: null pointer", fn);
+    return false;
+  }
+  if (fbs < 2LL * H * W && B > 1) {
+    set_error("%s: flow batch stride %lld < 2*H*W", fn, fbs);
+    return false;
+  }
+  return true;
+}
+
+int usf_splat_map_f32(const float* flow, long long flow_bstride, float* map, int B, int H, int W,
+                      int absolute, void* stream) {
+  clear_error();
+  if (!check_splat("usf_splat_map_f32", flow, flow_bstride, map, B, H, W)) return USF_EINVAL;
+  if (const int pe = pre_check("usf_splat_map_f32", (hipStream_t)stream)) return pe;
+  return finish("usf_splat_map_f32",
+                splat_launch(flow, flow_bstride, map, B, H, W, absolute != 0, (hipStream_t)stream),
+                (hipStream_t)stream);
+}
+
+int usf_occ_backward_f32(const float* flow21, long long flow_bstride, float* occ, int B, int H,
+                         int W, float th, void* stream) {
+  clear_error();
+  if (!check_splat("usf_occ_backward_f32", flow21, flow_bstride, occ, B, H, W)) return USF_EINVAL;
+  if (const int pe = pre_check("usf_occ_backward_f32", (hipStream_t)stream)) return pe;
+  return finish("usf_occ_backward_f32",
+                occ_backward_launch(flow21, flow_bstride, occ, B, H, W, th, (hipStream_t)stream),
+                (hipStream_t)stream);
+}
+
 int usf_set_variant(int op, int index) {
   clear_error();
   if (op < 0 || op > 2 || index < -1 || index >= variant_count(op)) {

@@ -33,4 +33,9 @@ hipError_t warp_bwd_launch(const float* x, const float* flow, long long flow_bst
                            const float* gout, float* gx, float* gflow, int B, int C, int H,
                            int W, int pad_mode, hipStream_t s);
 
+hipError_t splat_launch(const float* flow, long long flow_bstride, float* map, int B, int H, int W,
+                        bool absolute, hipStream_t s);
+hipError_t occ_backward_launch(const float* flow, long long flow_bstride, float* occ, int B, int H,
+                               int W, float th, hipStream_t s);
+
 }  // namespace usf

@@ -508,6 +508,63 @@ void bwd_launch_pad(const float* x, const float* flow, long long fbs, const floa
   }
 }
 
+// ----------------------------------------------------------- occlusion --
+// Forward bilinear splat of unit mass (warp_utils.py:26-94 get_corresponding_map,
+// used by get_occu_mask_backward :120-126): source pixel p of sample b lands at
+// (x, y) = (px + u, py + v) (ABS: (u, v) are absolute coordinates already) and
+// adds (1-|x-cx|)(1-|y-cy|) to each of its 4 integer neighbours (cx, cy) that
+// lies inside the image, with cx in {x0 = floor(x), x0 + 1}, computed in the
+// reference's fp32 order (contraction off). Same reduce-by-key scatter as the
+// warp's grad_x (lanes = consecutive source pixels): ~2 atomics per pixel.
+template <bool ABS>
+__global__ __launch_bounds__(256) void splat_kernel(const float* __restrict__ flow, long long fbs,
+                                                    float* __restrict__ map, int H, int W) {
+#pragma clang fp contract(off)
+  const int HW = H * W;
+  const int t = threadIdx.x;
+  const int lane = t & 63;
+  const int p = blockIdx.x * 256 + t;
+  const int b = blockIdx.y;
+  const bool valid = p < HW;
+  float x = 0.f, y = 0.f;
+  if (valid) {
+    const float* fb = flow + b * fbs;
+    const int py = p / W, px = p - py * W;
+    x = ABS ? fb[p] : (float)px + fb[p];
+    y = ABS ? fb[HW + p] : (float)py + fb[HW + p];
+  }
+  const float fx = floorf(x), fy = floorf(y);
+  const float fx1 = fx + 1.f, fy1 = fy + 1.f;
+  const float wm1 = (float)(W - 1), hm1 = (float)(H - 1);
+  // corner inside the image <=> clamp(c, 0, size-1) == c (the reference's test)
+  const bool vx0 = fx >= 0.f && fx <= wm1, vx1 = fx1 >= 0.f && fx1 <= wm1;
+  const bool vy0 = valid && fy >= 0.f && fy <= hm1, vy1 = valid && fy1 >= 0.f && fy1 <= hm1;
+  const float ax0 = 1.f - fabsf(x - fx), ax1 = 1.f - fabsf(x - fx1);
+  const float ay0 = 1.f - fabsf(y - fy), ay1 = 1.f - fabsf(y - fy1);
+  // integer corner indices, saturated so far-away targets cannot overflow
+  const int xi = fx < -1.f ? -2 : (fx > wm1 ? W : (int)fx);
+  const int yi = fy < -1.f ? -2 : (fy > hm1 ? H : (int)fy);
+  const bool kx = xi >= -1 && xi < W;  // keys alias nothing only for x0 in [-1, W-1]
+  const int kn = (vy0 && kx) ? yi * (W + 1) + xi + 1 : -(lane + 2);
+  const int ks = (vy1 && kx) ? (yi + 1) * (W + 1) + xi + 1 : -(lane + 2);
+  const bool has_left = lane != 0, has_right = lane != 63;
+  const bool m_nw = vx0 && vy0, m_ne = vx1 && vy0, m_sw = vx0 && vy1, m_se = vx1 && vy1;
+  const RowRuns rn = row_runs(kn, m_nw, m_ne, has_left, has_right);
+  const RowRuns rs = row_runs(ks, m_sw, m_se, has_left, has_right);
+  const int o_nw = m_nw || m_ne ? yi * W + xi : 0;
+  const int o_sw = m_sw || m_se ? (yi + 1) * W + xi : 0;
+  float* mb = map + (size_t)b * HW;
+  scatter_row(mb, o_nw, o_nw + 1, m_nw, m_ne, ax0 * ay0, ax1 * ay0, rn);
+  scatter_row(mb, o_sw, o_sw + 1, m_sw, m_se, ax0 * ay1, ax1 * ay1, rs);
+}
+
+// occ = clamp(map, 0, 1) < th ? 1 : 0, in place (get_occu_mask_backward :124-126)
+__global__ __launch_bounds__(256) void occ_threshold_kernel(float* __restrict__ m, long long n,
+                                                            float th) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) m[i] = fminf(fmaxf(m[i], 0.f), 1.f) < th ? 1.f : 0.f;
+}
+
 }  // namespace
 
 hipError_t warp_fwd_launch(const float* x, const float* flow, long long fbs, float* out, int B,
@@ -527,6 +584,28 @@ hipError_t warp_bwd_launch(const float* x, const float* flow, long long fbs, con
     bwd_launch_pad<true>(x, flow, fbs, gout, gx, gflow, B, C, H, W, s);
   else
     bwd_launch_pad<false>(x, flow, fbs, gout, gx, gflow, B, C, H, W, s);
+  return hipGetLastError();
+}
+
+hipError_t splat_launch(const float* flow, long long fbs, float* map, int B, int H, int W,
+                        bool absolute, hipStream_t s) {
+  hipError_t e = hipMemsetAsync(map, 0, (size_t)B * H * W * sizeof(float), s);
+  if (e != hipSuccess) return e;
+  const dim3 grid((unsigned)((H * W + 255) / 256), (unsigned)B);
+  if (absolute)
+    hipLaunchKernelGGL((splat_kernel<true>), grid, dim3(256), 0, s, flow, fbs, map, H, W);
+  else
+    hipLaunchKernelGGL((splat_kernel<false>), grid, dim3(256), 0, s, flow, fbs, map, H, W);
+  return hipGetLastError();
+}
+
+hipError_t occ_backward_launch(const float* flow, long long fbs, float* occ, int B, int H, int W,
+                               float th, hipStream_t s) {
+  hipError_t e = splat_launch(flow, fbs, occ, B, H, W, false, s);
+  if (e != hipSuccess) return e;
+  const long long n = (long long)B * H * W;
+  hipLaunchKernelGGL(occ_threshold_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, occ, n,
+                     th);
   return hipGetLastError();
 }
 

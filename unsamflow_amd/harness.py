@@ -59,17 +59,21 @@ class TrainStep:
     """One PWCLite fwd(with_bk) + unFlowLoss + bwd + clip + Adam + OneCycleLR step."""
 
     def __init__(self, cfg, device, ddp: bool = False, corr_module=None, warp_fn: Callable | None = None,
-                 loss_kwargs: dict | None = None, fused_adam: bool | None = None, seed: int = 42):
+                 loss_kwargs: dict | None = None, fused_adam: bool | None = None, seed: int = 42,
+                 channels_last: bool = False, occ_backward_fn: Callable | None = None):
         torch.manual_seed(seed)
         self.cfg = cfg
         self.device = torch.device(device)
         model = PWCLite(cfg.model, corr_module=corr_module, warp_fn=warp_fn).to(self.device)
+        if channels_last:  # NHWC weights/activations for MIOpen's NHWC convolutions
+            model = model.to(memory_format=torch.channels_last)
         self.module = model
         if ddp:
             ids = [self.device.index] if self.device.type == "cuda" else None
             model = torch.nn.parallel.DistributedDataParallel(model, device_ids=ids)
         self.model = model
-        self.loss_fn = unFlowLoss(cfg.loss, warp_fn=warp_fn, **(loss_kwargs or {}))
+        self.loss_fn = unFlowLoss(cfg.loss, warp_fn=warp_fn, occ_backward_fn=occ_backward_fn,
+                                  **(loss_kwargs or {}))
         t = cfg.train
         if fused_adam is None:
             fused_adam = self.device.type == "cuda"
@@ -107,13 +111,14 @@ def smoke_step(device) -> None:
     """Tiny PWCLite step on ``device`` checked against the same model on CPU with
     the oracle ops (hash-initialised weights, 64x128, B=1)."""
     from oracle.hashrng import hash_init_, uniform
-    from oracle.torch_ref import OracleCorrelation, oracle_flow_warp
+    from oracle.torch_ref import OracleCorrelation, oracle_flow_warp, oracle_occu_mask_backward
 
     from .config import kitti_base
 
     cfg = kitti_base()
     gpu = TrainStep(cfg, device)
-    cpu = TrainStep(kitti_base(), "cpu", corr_module=OracleCorrelation(4), warp_fn=oracle_flow_warp)
+    cpu = TrainStep(kitti_base(), "cpu", corr_module=OracleCorrelation(4), warp_fn=oracle_flow_warp,
+                    occ_backward_fn=oracle_occu_mask_backward)
     hash_init_(gpu.module, seed=1)
     hash_init_(cpu.module, seed=1)
     im1 = torch.from_numpy(uniform((1, 3, 64, 128), 11))

@@ -189,3 +189,41 @@ def warp_backward(
         )
     _lib.check(rc, "usf_warp_bwd_f32")
     return gx, gf
+
+
+def _flow_arg(flow: torch.Tensor, name: str) -> tuple[torch.Tensor, int, int, int, int]:
+    _require_device_f32(name, flow)
+    if flow.dim() != 4 or flow.shape[1] != 2:
+        raise ValueError(f"{name} must be [B,2,H,W], got {tuple(flow.shape)}")
+    B, _, H, W = flow.shape
+    fv, fbs = _flow_view(flow, B, H, W)
+    return fv, fbs, B, H, W
+
+
+def splat_map(flow: torch.Tensor, absolute: bool = False) -> torch.Tensor:
+    """Forward bilinear splat of unit mass (warp_utils.py:26-94) -> [B,1,H,W].
+
+    ``absolute``: ``flow`` holds target coordinates (get_corresponding_map's
+    argument) instead of displacements from the pixel grid."""
+    fv, fbs, B, H, W = _flow_arg(flow, "flow")
+    out = torch.empty((B, 1, H, W), device=flow.device, dtype=torch.float32)
+    lib = _lib.load()
+    with torch.cuda.device(flow.device), _kt.timed("splat", (B, 1, H, W, bool(absolute)), flow.device,
+                                                     4 * B * H * W * 3):
+        rc = lib.usf_splat_map_f32(fv.data_ptr(), fbs, out.data_ptr(), B, H, W, int(bool(absolute)),
+                                   _lib.stream_handle(flow.device))
+    _lib.check(rc, "usf_splat_map_f32")
+    return out
+
+
+def occ_backward(flow21: torch.Tensor, th: float = 0.2) -> torch.Tensor:
+    """Occlusion mask get_occu_mask_backward (warp_utils.py:120-126) -> [B,1,H,W] float."""
+    fv, fbs, B, H, W = _flow_arg(flow21, "flow21")
+    out = torch.empty((B, 1, H, W), device=flow21.device, dtype=torch.float32)
+    lib = _lib.load()
+    with torch.cuda.device(flow21.device), _kt.timed("occ_bwd", (B, 1, H, W), flow21.device,
+                                                       4 * B * H * W * 3):
+        rc = lib.usf_occ_backward_f32(fv.data_ptr(), fbs, out.data_ptr(), B, H, W, float(th),
+                                      _lib.stream_handle(flow21.device))
+    _lib.check(rc, "usf_occ_backward_f32")
+    return out

@@ -10,11 +10,13 @@ kernels, plus the reference's grid helpers and occlusion estimators.
 * ``mesh_grid`` / ``norm_grid`` (:7-23) keep their reference semantics
   (int64 grid, [B,H,W,2] normalised grid); ``mesh_grid`` builds on the
   requested device instead of always on the CPU.
-* ``get_corresponding_map`` / ``get_occu_mask_backward`` /
-  ``get_occu_mask_bidirection`` (:26-94, :109-126) are the occlusion
-  estimators the loss uses (no gradient flows through them). They are
-  composed from torch ops here (the bidirectional one calls the HIP warp);
-  a dedicated splat kernel is a listed next step.
+* ``get_corresponding_map`` / ``get_occu_mask_backward`` (:26-94, :120-126)
+  run the HIP forward-splat kernel (``usf_splat_map_f32`` /
+  ``usf_occ_backward_f32``: reduce-by-key fp32 atomics, threshold fused in
+  place) instead of ~20 torch ops and an int64 ``scatter_add_``;
+  ``get_occu_mask_bidirection`` (:109-117) is the HIP zeros-padded warp plus
+  elementwise torch ops. No gradient flows through the masks (the reference
+  thresholds them).
 """
 from __future__ import annotations
 
@@ -64,45 +66,16 @@ def flow_warp(x: torch.Tensor, flow12: torch.Tensor, pad: str = "border", mode: 
 
 
 def get_corresponding_map(data: torch.Tensor) -> torch.Tensor:
-    """Forward-splat of unit mass along ``data`` (unnormalised coords [B,2,H,W]) -> [B,1,H,W].
-
-    Each source pixel spreads bilinear weights to the 4 integer neighbours of
-    its target; corners outside the image are dropped (warp_utils.py:26-94).
-    """
-    B, _, H, W = data.size()
-    x = data[:, 0].reshape(B, -1)
-    y = data[:, 1].reshape(B, -1)
-    x0 = torch.floor(x)
-    y0 = torch.floor(y)
-    x1 = x0 + 1
-    y1 = y0 + 1
-    xw = x0.clamp(0, W - 1)
-    yn = y0.clamp(0, H - 1)
-    xe = x1.clamp(0, W - 1)
-    ys = y1.clamp(0, H - 1)
-    out = torch.zeros(B, H * W, dtype=data.dtype, device=data.device)
-    # (x corner, y corner, x inside?, y inside?) in the reference's concat order
-    corners = (
-        (xe, ys, x1 == xe, y1 == ys),
-        (xe, yn, x1 == xe, y0 == yn),
-        (xw, ys, x0 == xw, y1 == ys),
-        (xw, yn, x0 == xw, y0 == yn),
-    )
-    idx, val = [], []
-    for cx, cy, okx, oky in corners:
-        wgt = (1 - torch.abs(x - cx)) * (1 - torch.abs(y - cy))
-        idx.append(cx + cy * W)
-        val.append(torch.where(okx & oky, wgt, torch.zeros_like(wgt)))
-    out.scatter_add_(1, torch.cat(idx, 1).long(), torch.cat(val, 1))
-    return out.view(B, 1, H, W)
+    """Forward-splat of unit mass along ``data`` (unnormalised target coords
+    [B,2,H,W]) -> [B,1,H,W] (warp_utils.py:26-94): each source pixel spreads
+    bilinear weights to the 4 integer neighbours of its target; corners
+    outside the image are dropped."""
+    return ops.splat_map(data, absolute=True)
 
 
 def get_occu_mask_backward(flow21: torch.Tensor, th: float = 0.2) -> torch.Tensor:
     """1 where nothing in frame 2 maps onto the pixel (occluded), else 0 (:120-126)."""
-    B, _, H, W = flow21.size()
-    base = mesh_grid(B, H, W, device=flow21.device).type_as(flow21)
-    corr_map = get_corresponding_map(base + flow21)
-    return (corr_map.clamp(min=0.0, max=1.0) < th).float()
+    return ops.occ_backward(flow21, th)
 
 
 def get_occu_mask_bidirection(flow12: torch.Tensor, flow21: torch.Tensor, scale: float = 0.01,
