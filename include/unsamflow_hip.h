@@ -21,6 +21,8 @@
  *                        scatter_add_ of bilinear weights)
  *   usf_occ_backward_f32 <- get_occu_mask_backward (warp_utils.py:120-126),
  *                        caller losses/flow_loss.py:101-103 (occ_from_back)
+ *   usf_photo_loss_*  <- the per-scale warp + loss_photomatric composition of
+ *                        losses/flow_loss.py:127-148
  *
  * Contract (all entry points):
  *   - Pointers are DEVICE pointers to fp32 NCHW tensors. x/x1/x2/gout/out/gx*
@@ -111,6 +113,31 @@ int usf_splat_map_f32(const float* flow, long long flow_bstride, float* map,
  * occ: [B,1,H,W] dense, overwritten. */
 int usf_occ_backward_f32(const float* flow21, long long flow_bstride, float* occ,
                          int B, int H, int W, float th, void* stream);
+
+/* Fused occlusion-aware photometric loss of one scale and direction
+ * (losses/flow_loss.py:127-148, loss_photomatric :33-50, SSIM
+ * losses/loss_blocks.py:53-72, w_ternary = 0):
+ *   rec = flow_warp(src, flow, pad_mode)
+ *   L = (w_l1 * mean |tgt - rec| * m + w_ssim * mean SSIM(rec*m, tgt*m))
+ *       / (mean m + 1e-6)
+ * src, tgt: [B,C,H,W] dense, 1 <= C <= 4; mask: [B,1,H,W] dense; flow:
+ * [B,2,H,W] with batch stride flow_bstride. partials: caller scratch of
+ * usf_photo_loss_partials(B,H,W) floats. out: 3 floats = {L, c_l1, c_ssim}
+ * (c_* are what the backward needs). Deterministic (fixed-order sums). */
+int usf_photo_loss_partials(int B, int H, int W);
+int usf_photo_loss_fwd_f32(const float* src, const float* tgt, const float* mask,
+                           const float* flow, long long flow_bstride, float* partials,
+                           float* out, int B, int C, int H, int W, int pad_mode,
+                           float w_l1, float w_ssim, void* stream);
+
+/* Backward of usf_photo_loss_fwd_f32 w.r.t. the flow only (the mask and the
+ * images carry no gradient): grad_flow = dL/dflow * (*grad_loss).
+ * coef: the `out` of the forward (device pointer); grad_loss: device scalar;
+ * grad_flow: [B,2,H,W] dense, overwritten, deterministic. */
+int usf_photo_loss_bwd_f32(const float* src, const float* tgt, const float* mask,
+                           const float* flow, long long flow_bstride, const float* coef,
+                           const float* grad_loss, float* grad_flow, int B, int C, int H,
+                           int W, int pad_mode, void* stream);
 
 /* Tuning hook (benchmarking only; not needed for correct use).
  * Forces kernel variant `index` of `op` for d=4 launches in this process:

@@ -1,0 +1,89 @@
+"""Fused photometric loss (unsamflow_amd.photometric, csrc/photo.hip) vs the
+reference composition on the CPU: oracle flow_warp (grid_sample) + the torch
+L1/SSIM of loss_photomatric (flow_loss.py:33-50, loss_blocks.py:53-72), fp32.
+Loss value: rtol 2e-5. grad_flow: atol 2e-4 x max|grad| + rtol 1e-3 (the
+backward sums the 9 SSIM windows and the channels in another order)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import hashrng
+from oracle.torch_ref import oracle_flow_warp
+
+pytestmark = pytest.mark.gpu
+
+
+def _ref_loss(flow, src, tgt, mask, pad, w_l1, w_ssim):
+    from unsamflow_amd.config import AttrDict
+    from unsamflow_amd.flow_loss import unFlowLoss
+
+    cfg = AttrDict.wrap(dict(w_l1=w_l1, w_ssim=w_ssim, w_ternary=0.0))
+    lf = unFlowLoss(cfg, warp_fn=oracle_flow_warp)
+    rec = oracle_flow_warp(src, flow, pad=pad)
+    return lf.loss_photomatric(tgt, rec, mask)
+
+
+CASES = [
+    # (B, C, H, W, flow scale, mask kind, pad)
+    (2, 3, 24, 40, 2.0, "rand", "border"),
+    (2, 3, 17, 29, 6.0, "ones", "border"),
+    (1, 3, 3, 5, 1.0, "rand", "border"),
+    (2, 3, 33, 47, 3.0, "rand", "zeros"),
+    (2, 1, 20, 36, 2.0, "rand", "border"),
+    (8, 3, 64, 208, 4.0, "rand", "border"),
+]
+
+
+@pytest.mark.parametrize("B,C,H,W,scale,mkind,pad", CASES)
+def test_photometric_loss_matches_reference_composition(hip_device, B, C, H, W, scale, mkind, pad):
+    from unsamflow_amd.photometric import photometric_loss
+
+    seed = 100 + H + W
+    src = torch.from_numpy(hashrng.uniform((B, C, H, W), seed))
+    tgt = torch.from_numpy(hashrng.uniform((B, C, H, W), seed + 1))
+    flow_full = torch.from_numpy(hashrng.symmetric((B, 4, H, W), seed + 2, scale))
+    if mkind == "ones":
+        mask = torch.ones(B, 1, H, W)
+    else:
+        mask = (torch.from_numpy(hashrng.uniform((B, 1, H, W), seed + 3)) > 0.2).float()
+
+    fr = flow_full.clone().requires_grad_(True)
+    ref = _ref_loss(fr[:, :2], src, tgt, mask, pad, 0.15, 0.85)
+    ref.backward()
+    gref = fr.grad[:, :2].numpy()
+
+    fd = flow_full.to(hip_device).requires_grad_(True)
+    out = photometric_loss(fd[:, :2], src.to(hip_device), tgt.to(hip_device), mask.to(hip_device), pad,
+                           0.15, 0.85)
+    out.backward()
+    g = fd.grad[:, :2].cpu().numpy()
+    assert float(fd.grad[:, 2:].abs().max()) == 0.0
+    np.testing.assert_allclose(float(out), float(ref), rtol=2e-5, atol=0)
+    np.testing.assert_allclose(g, gref, rtol=1e-3, atol=2e-4 * float(np.abs(gref).max()))
+
+
+def test_photometric_loss_in_unflowloss_matches_torch_path(hip_device):
+    """unFlowLoss with the fused op == unFlowLoss with the library warp + torch
+    L1/SSIM (fused_photometric=False), value and flow gradients, at the KITTI
+    loss pyramid (4 scales, B=2, 256x832 top)."""
+    from unsamflow_amd.config import kitti_base
+    from unsamflow_amd.flow_loss import unFlowLoss
+
+    cfg = kitti_base().loss
+    B = 2
+    img1 = torch.from_numpy(hashrng.uniform((B, 3, 256, 832), 11)).to(hip_device)
+    img2 = torch.from_numpy(hashrng.uniform((B, 3, 256, 832), 12)).to(hip_device)
+    flows = [torch.from_numpy(hashrng.symmetric((B, 4, 256 >> i, 832 >> i), 20 + i, 3.0 / (1 << i)))
+             for i in range(5)]
+    res = []
+    for fused in (True, False):
+        fl = [f.to(hip_device).requires_grad_(True) for f in flows]
+        loss = unFlowLoss(cfg, fused_photometric=fused)(fl, img1, img2)[0].sum()
+        loss.backward()
+        res.append((float(loss), [None if f.grad is None else f.grad.cpu().numpy() for f in fl]))
+    (lf, gf), (lt, gt) = res
+    np.testing.assert_allclose(lf, lt, rtol=2e-5)
+    for a, b in zip(gf, gt):  # the 5th level has photometric weight 0 (no gradient at all)
+        assert (a is None) == (b is None)
+        if a is not None:
+            np.testing.assert_allclose(a, b, rtol=1e-3, atol=2e-4 * max(float(np.abs(b).max()), 1e-12))

@@ -52,6 +52,16 @@ _SIGNATURES = {
         [_c_float_p, ctypes.c_longlong, _c_float_p] + [ctypes.c_int] * 3 + [ctypes.c_float, ctypes.c_void_p],
         ctypes.c_int,
     ),
+    "usf_photo_loss_partials": ([ctypes.c_int] * 3, ctypes.c_int),
+    "usf_photo_loss_fwd_f32": (
+        [_c_float_p] * 4 + [ctypes.c_longlong, _c_float_p, _c_float_p] + [ctypes.c_int] * 5
+        + [ctypes.c_float, ctypes.c_float, ctypes.c_void_p],
+        ctypes.c_int,
+    ),
+    "usf_photo_loss_bwd_f32": (
+        [_c_float_p] * 4 + [ctypes.c_longlong] + [_c_float_p] * 3 + [ctypes.c_int] * 5 + [ctypes.c_void_p],
+        ctypes.c_int,
+    ),
     "usf_set_variant": ([ctypes.c_int, ctypes.c_int], ctypes.c_int),
 }
 EXPORTED_SYMBOLS = tuple(_SIGNATURES)

@@ -199,6 +199,66 @@ int usf_occ_backward_f32(const float* flow21, long long flow_bstride, float* occ
                 (hipStream_t)stream);
 }
 
+int usf_photo_loss_partials(int B, int H, int W) {
+  return (B > 0 && H > 0 && W > 0) ? photo_partials(B, H, W) : 0;
+}
+
+static bool check_photo(const char* fn, const float* src, const float* tgt, const float* mask,
+                        const float* flow, long long fbs, int B, int C, int H, int W, int pad_mode) {
+  if (!check_dims(fn, B, C, H, W)) return false;
+  if (C > 4) {
+    set_error("%s: C=%d image channels > 4", fn, C);
+    return false;
+  }
+  if (pad_mode != USF_PAD_ZEROS && pad_mode != USF_PAD_BORDER) {
+    set_error("%s: unknown pad_mode %d", fn, pad_mode);
+    return false;
+  }
+  if (!src || !tgt || !mask || !flow) {
+    set_error("%s: null input pointer", fn);
+    return false;
+  }
+  if (fbs < 2LL * H * W && B > 1) {
+    set_error("%s: flow batch stride %lld < 2*H*W", fn, fbs);
+    return false;
+  }
+  return true;
+}
+
+int usf_photo_loss_fwd_f32(const float* src, const float* tgt, const float* mask, const float* flow,
+                           long long flow_bstride, float* partials, float* out, int B, int C, int H,
+                           int W, int pad_mode, float w_l1, float w_ssim, void* stream) {
+  clear_error();
+  if (!check_photo("usf_photo_loss_fwd_f32", src, tgt, mask, flow, flow_bstride, B, C, H, W, pad_mode))
+    return USF_EINVAL;
+  if (!partials || !out) {
+    set_error("usf_photo_loss_fwd_f32: null output pointer");
+    return USF_EINVAL;
+  }
+  if (const int pe = pre_check("usf_photo_loss_fwd_f32", (hipStream_t)stream)) return pe;
+  return finish("usf_photo_loss_fwd_f32",
+                photo_fwd_launch(src, tgt, mask, flow, flow_bstride, partials, out, B, C, H, W,
+                                 pad_mode, w_l1, w_ssim, (hipStream_t)stream),
+                (hipStream_t)stream);
+}
+
+int usf_photo_loss_bwd_f32(const float* src, const float* tgt, const float* mask, const float* flow,
+                           long long flow_bstride, const float* coef, const float* grad_loss,
+                           float* grad_flow, int B, int C, int H, int W, int pad_mode, void* stream) {
+  clear_error();
+  if (!check_photo("usf_photo_loss_bwd_f32", src, tgt, mask, flow, flow_bstride, B, C, H, W, pad_mode))
+    return USF_EINVAL;
+  if (!coef || !grad_loss || !grad_flow) {
+    set_error("usf_photo_loss_bwd_f32: null pointer");
+    return USF_EINVAL;
+  }
+  if (const int pe = pre_check("usf_photo_loss_bwd_f32", (hipStream_t)stream)) return pe;
+  return finish("usf_photo_loss_bwd_f32",
+                photo_bwd_launch(src, tgt, mask, flow, flow_bstride, coef, grad_loss, grad_flow, B, C,
+                                 H, W, pad_mode, (hipStream_t)stream),
+                (hipStream_t)stream);
+}
+
 int usf_set_variant(int op, int index) {
   clear_error();
   if (op < 0 || op > 2 || index < -1 || index >= variant_count(op)) {

@@ -38,4 +38,12 @@ hipError_t splat_launch(const float* flow, long long flow_bstride, float* map, i
 hipError_t occ_backward_launch(const float* flow, long long flow_bstride, float* occ, int B, int H,
                                int W, float th, hipStream_t s);
 
+int photo_partials(int B, int H, int W);
+hipError_t photo_fwd_launch(const float* src, const float* tgt, const float* mask, const float* flow,
+                            long long flow_bstride, float* partials, float* out, int B, int C, int H,
+                            int W, int pad_mode, float w_l1, float w_ssim, hipStream_t s);
+hipError_t photo_bwd_launch(const float* src, const float* tgt, const float* mask, const float* flow,
+                            long long flow_bstride, const float* coef, const float* gloss,
+                            float* gflow, int B, int C, int H, int W, int pad_mode, hipStream_t s);
+
 }  // namespace usf

@@ -9,6 +9,10 @@ the bidirectional check), nearest-resized per scale; per scale with
 two flow halves (``flow[:, :2]`` / ``flow[:, 2:]``, :130-131), occlusion-aware
 photometric loss (L1 + SSIM + ternary, :33-50) averaged over the two
 directions; edge-aware 1st/2nd-order smoothness at scale 0 when ``w_sm > 0``.
+On a ROCm device with the library's warp and ``w_ternary == 0`` the warp +
+L1 + SSIM of each scale and direction is one fused autograd op
+(unsamflow_amd.photometric); ``fused_photometric=False``
+or an injected ``warp_fn`` keeps the torch composition.
 Returns ``(loss[None], l_ph[None], l_sm[None], flow_mean[None], vis1, vis2)``.
 
 ``smooth_type == "homography"`` needs OpenCV RANSAC on the host
@@ -99,7 +103,7 @@ def _default_warp():
 
 class unFlowLoss(nn.Module):  # noqa: N801 (reference name)
     def __init__(self, cfg, warp_fn: Callable | None = None, occ_backward_fn: Callable | None = None,
-                 occ_bidir_fn: Callable | None = None):
+                 occ_bidir_fn: Callable | None = None, fused_photometric: bool = True):
         super().__init__()
         self.cfg = cfg
         if "ransac_threshold" not in cfg:
@@ -107,8 +111,17 @@ class unFlowLoss(nn.Module):  # noqa: N801 (reference name)
         from . import warp_utils
 
         self.warp = warp_fn if warp_fn is not None else _default_warp()
+        # fused photometric kernels only behind the library's own warp (an injected
+        # warp -- e.g. the CPU oracle -- keeps the torch composition below)
+        self.fused = warp_fn is None and fused_photometric
         self.occ_backward = occ_backward_fn or warp_utils.get_occu_mask_backward
         self.occ_bidir = occ_bidir_fn or (lambda f12, f21: warp_utils.get_occu_mask_bidirection(f12, f21))
+
+    def _fused_photometric(self, flow) -> bool:
+        """Fused HIP warp+L1+SSIM (unsamflow_amd.photometric) when this loss uses the
+        library's own warp on a ROCm device and the photometric terms are L1/SSIM."""
+        c = self.cfg
+        return (self.fused and flow.is_cuda and c.w_ternary == 0 and c.w_l1 >= 0 and c.w_ssim >= 0)
 
     def loss_photomatric(self, im1_scaled, im1_recons, vis_mask1):
         c = self.cfg
@@ -152,16 +165,24 @@ class unFlowLoss(nn.Module):  # noqa: N801 (reference name)
             if c.w_ph_scales[i] > 0:
                 im1_s = F.interpolate(im1_origin, (h, w), mode="area")
                 im2_s = F.interpolate(im2_origin, (h, w), mode="area")
-                im1_rec = self.warp(im2_s, flow[:, :2], pad=c.warp_pad)
-                im2_rec = self.warp(im1_s, flow[:, 2:], pad=c.warp_pad)
                 if occ_aware:
                     m1, m2 = vis1_pyr[i], vis2_pyr[i]
                 else:
                     m1 = torch.ones((b, 1, h, w), dtype=torch.float32, device=dev)
                     m2 = torch.ones((b, 1, h, w), dtype=torch.float32, device=dev)
-                lw = self.loss_photomatric(im1_s, im1_rec, m1)
-                if c.with_bk:
-                    lw = (lw + self.loss_photomatric(im2_s, im2_rec, m2)) / 2.0
+                if self._fused_photometric(flow):
+                    from .photometric import photometric_loss
+
+                    lw = photometric_loss(flow[:, :2], im2_s, im1_s, m1, c.warp_pad, c.w_l1, c.w_ssim)
+                    if c.with_bk:
+                        lw = (lw + photometric_loss(flow[:, 2:], im1_s, im2_s, m2, c.warp_pad, c.w_l1,
+                                                    c.w_ssim)) / 2.0
+                else:
+                    im1_rec = self.warp(im2_s, flow[:, :2], pad=c.warp_pad)
+                    im2_rec = self.warp(im1_s, flow[:, 2:], pad=c.warp_pad)
+                    lw = self.loss_photomatric(im1_s, im1_rec, m1)
+                    if c.with_bk:
+                        lw = (lw + self.loss_photomatric(im2_s, im2_rec, m2)) / 2.0
                 warp_losses.append(lw)
             else:
                 warp_losses.append(zero)

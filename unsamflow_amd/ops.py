@@ -227,3 +227,50 @@ def occ_backward(flow21: torch.Tensor, th: float = 0.2) -> torch.Tensor:
                                       _lib.stream_handle(flow21.device))
     _lib.check(rc, "usf_occ_backward_f32")
     return out
+
+
+def _photo_args(src, tgt, mask, flow):
+    for n, t in (("src", src), ("tgt", tgt), ("mask", mask)):
+        _require_device_f32(n, t)
+    B, C, H, W = _nchw("src", src)
+    if tuple(tgt.shape) != (B, C, H, W) or tuple(mask.shape) != (B, 1, H, W):
+        raise ValueError(f"tgt {tuple(tgt.shape)} / mask {tuple(mask.shape)} do not match src {(B, C, H, W)}")
+    if C > 4:
+        raise NotImplementedError(f"fused photometric loss supports C <= 4 image channels, got {C}")
+    _require_device_f32("flow", flow)
+    fv, fbs = _flow_view(flow, B, H, W)
+    return src.contiguous(), tgt.contiguous(), mask.contiguous(), fv, fbs, B, C, H, W
+
+
+def photo_loss_forward(src, tgt, mask, flow, pad: str = "border", w_l1: float = 0.15, w_ssim: float = 0.85):
+    """Fused warp + occlusion-aware L1/SSIM photometric loss of one scale and
+    direction (flow_loss.py:127-148, loss_blocks.py:53-72) -> tensor [3] on the
+    device: {loss, c_l1, c_ssim} (the last two feed the backward)."""
+    if pad not in PAD_MODES:
+        raise NotImplementedError(f"flow_warp padding mode {pad!r} (supported: border, zeros)")
+    s, t, m, fv, fbs, B, C, H, W = _photo_args(src, tgt, mask, flow)
+    lib = _lib.load()
+    partials = torch.empty(lib.usf_photo_loss_partials(B, H, W), device=src.device, dtype=torch.float32)
+    out = torch.empty(3, device=src.device, dtype=torch.float32)
+    with torch.cuda.device(src.device), _kt.timed("photo_fwd", (B, C, H, W, pad), src.device,
+                                                    4 * B * H * W * (2 * C + 3)):
+        rc = lib.usf_photo_loss_fwd_f32(s.data_ptr(), t.data_ptr(), m.data_ptr(), fv.data_ptr(), fbs,
+                                        partials.data_ptr(), out.data_ptr(), B, C, H, W, PAD_MODES[pad],
+                                        float(w_l1), float(w_ssim), _lib.stream_handle(src.device))
+    _lib.check(rc, "usf_photo_loss_fwd_f32")
+    return out
+
+
+def photo_loss_backward(src, tgt, mask, flow, coef, grad_loss, pad: str = "border"):
+    """d(photo loss)/d(flow) * grad_loss -> [B,2,H,W] (deterministic)."""
+    s, t, m, fv, fbs, B, C, H, W = _photo_args(src, tgt, mask, flow)
+    gl = grad_loss.reshape(1).to(torch.float32).contiguous()
+    gflow = torch.empty((B, 2, H, W), device=src.device, dtype=torch.float32)
+    lib = _lib.load()
+    with torch.cuda.device(src.device), _kt.timed("photo_bwd", (B, C, H, W, pad), src.device,
+                                                    4 * B * H * W * (2 * C + 5)):
+        rc = lib.usf_photo_loss_bwd_f32(s.data_ptr(), t.data_ptr(), m.data_ptr(), fv.data_ptr(), fbs,
+                                        coef.data_ptr(), gl.data_ptr(), gflow.data_ptr(), B, C, H, W,
+                                        PAD_MODES[pad], _lib.stream_handle(src.device))
+    _lib.check(rc, "usf_photo_loss_bwd_f32")
+    return gflow
