@@ -120,7 +120,7 @@ int usf_occ_backward_f32(const float* flow21, long long flow_bstride, float* occ
  *   rec = flow_warp(src, flow, pad_mode)
  *   L = (w_l1 * mean |tgt - rec| * m + w_ssim * mean SSIM(rec*m, tgt*m))
  *       / (mean m + 1e-6)
- * src, tgt: [B,C,H,W] dense, 1 <= C <= 4; mask: [B,1,H,W] dense; flow:
+ * src, tgt: [B,C,H,W] dense, 1 <= C <= 3 (images); mask: [B,1,H,W] dense; flow:
  * [B,2,H,W] with batch stride flow_bstride. partials: caller scratch of
  * usf_photo_loss_partials(B,H,W) floats. out: 3 floats = {L, c_l1, c_ssim}
  * (c_* are what the backward needs). Deterministic (fixed-order sums). */

@@ -80,7 +80,7 @@ def test_no_torch_types_in_abi():
         (lambda L: L.usf_splat_map_f32(None, 2 * 16, 1, 1, 4, 4, 0, None), "null pointer"),
         (lambda L: L.usf_occ_backward_f32(1, 3, 1, 2, 4, 4, 0.2, None), "batch stride"),
         (lambda L: L.usf_occ_backward_f32(1, 32, None, 1, 4, 4, 0.2, None), "null pointer"),
-        (lambda L: L.usf_photo_loss_fwd_f32(1, 1, 1, 1, 32, 1, 1, 1, 5, 4, 4, 1, 0.15, 0.85, None), "> 4"),
+        (lambda L: L.usf_photo_loss_fwd_f32(1, 1, 1, 1, 32, 1, 1, 1, 4, 4, 4, 1, 0.15, 0.85, None), "> 3"),
         (lambda L: L.usf_photo_loss_fwd_f32(1, 1, 1, 1, 32, 1, 1, 1, 3, 4, 4, 9, 0.15, 0.85, None), "pad_mode 9"),
         (lambda L: L.usf_photo_loss_fwd_f32(1, None, 1, 1, 32, 1, 1, 1, 3, 4, 4, 1, 0.15, 0.85, None), "null input"),
         (lambda L: L.usf_photo_loss_bwd_f32(1, 1, 1, 1, 32, None, 1, 1, 1, 3, 4, 4, 1, None), "null pointer"),

@@ -17,6 +17,9 @@ SITES += [("corr_bwd", (8, C, H, W, True, True)) for C, H, W in KITTI]
 SITES += [("warp_fwd", (8, C, H, W, "border")) for C, H, W in KITTI[1:]]
 SITES += [("warp_bwd", (8, C, H, W, "border", True, True)) for C, H, W in KITTI[1:]]
 SITES += [("warp_fwd", (8, 3, 256, 832, "border")), ("warp_bwd", (8, 3, 256, 832, "border", False, True))]
+SITES += [("occ_bwd", (8, 1, 256, 832))]
+SITES += [("photo_fwd", (8, 3, 256 >> i, 832 >> i, "border")) for i in range(4)]
+SITES += [("photo_bwd", (8, 3, 256 >> i, 832 >> i, "border")) for i in range(4)]
 
 
 def main():

@@ -206,8 +206,8 @@ int usf_photo_loss_partials(int B, int H, int W) {
 static bool check_photo(const char* fn, const float* src, const float* tgt, const float* mask,
                         const float* flow, long long fbs, int B, int C, int H, int W, int pad_mode) {
   if (!check_dims(fn, B, C, H, W)) return false;
-  if (C > 4) {
-    set_error("%s: C=%d image channels > 4", fn, C);
+  if (C > 3) {
+    set_error("%s: C=%d image channels > 3", fn, C);
     return false;
   }
   if (pad_mode != USF_PAD_ZEROS && pad_mode != USF_PAD_BORDER) {

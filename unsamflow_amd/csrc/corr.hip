@@ -207,27 +207,6 @@ struct Layout {
   __device__ static int seg(int lane) { return COLMAJOR ? lane / TH : lane % SEGX; }
 };
 
-// Workgroups are dealt round-robin over the 8 XCDs, so blocks b and b + 8 share
-// an L2 (MI355X_MICROARCH.md §Workgroup dispatch; a speed property, never a
-// correctness one). Renumber the linear block id so that CONSECUTIVE work items
-// -- which share staged data (a tile's displacement-row groups / channel
-// groups, neighbouring tiles' halos) -- run on one XCD. Bijective on [0, n).
-// Used by the forward kernel (L3 16.7 vs 18.6 us, FETCH traffic 3.9x -> 1.0x of
-// algorithmic). USF_XCD_REMAP=0 (tools/ab_build.py A/B builds) turns it off.
-#ifndef USF_XCD_REMAP
-#define USF_XCD_REMAP 1
-#endif
-__device__ __forceinline__ int xcd_remap(int lin, int n) {
-  if (!USF_XCD_REMAP) return lin;
-  const int full = n & ~7;
-  if (lin >= full) return lin;
-  return (lin & 7) * (full >> 3) + (lin >> 3);
-}
-
-__device__ __forceinline__ int linear_block() {
-  return blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
-}
-
 // One stage of CC channel planes staged HBM -> LDS: plane c of the stage is
 // a ROWS x S image (row stride S, COLS valid columns from global column gx0,
 // rows from gy0) at LDS offset c * PL, PL = ROWS * S rounded up to whole DMA

@@ -31,7 +31,7 @@ namespace usf {
 namespace {
 
 constexpr int kTile = 16;              // 16x16 output pixels per workgroup (256 threads)
-constexpr int kMaxC = 4;               // image channels held per pixel (3 = RGB)
+constexpr int kMaxC = 3;               // image channels per pixel (RGB; LDS is sized for 3)
 constexpr float kC1 = 0.01f * 0.01f;   // torch casts the python scalars to fp32
 constexpr float kC2 = 0.03f * 0.03f;
 
@@ -55,6 +55,17 @@ __device__ __forceinline__ void sample_px(const float* __restrict__ srcb, const 
     const float vse = tp.m_se ? sc[tp.o_se] : 0.f;
     out[c] = vnw * wnw + vne * wne + vsw * wsw + vse * wse;  // ATen's order
   }
+}
+
+// tile and sample of this workgroup: grid = (tiles, B), XCD-aware order so that
+// neighbouring tiles (shared halos and gather footprints) run on one L2
+__device__ __forceinline__ void photo_work(int tiles_x, int& ty0, int& tx0, int& b) {
+  const int ntiles = gridDim.x;
+  const int w = xcd_remap(linear_block(), ntiles * gridDim.y);
+  const int tile = w % ntiles;
+  b = w / ntiles;
+  ty0 = (tile / tiles_x) * kTile;
+  tx0 = (tile % tiles_x) * kTile;
 }
 
 // block-wide sum of 3 values in a fixed order (deterministic)
@@ -92,8 +103,8 @@ __global__ __launch_bounds__(256) void photo_fwd_kernel(const float* __restrict_
   __shared__ float xs[kMaxC][R][R + 1], ys[kMaxC][R][R + 1];
   __shared__ float red[768];
   const int t = threadIdx.x;
-  const int b = blockIdx.y;
-  const int ty0 = (blockIdx.x / tiles_x) * kTile, tx0 = (blockIdx.x % tiles_x) * kTile;
+  int ty0, tx0, b;
+  photo_work(tiles_x, ty0, tx0, b);
   const int HW = H * W;
   const float* srcb = src + (size_t)b * C * HW;
   const float* tgtb = tgt + (size_t)b * C * HW;
@@ -104,7 +115,7 @@ __global__ __launch_bounds__(256) void photo_fwd_kernel(const float* __restrict_
   for (int e = t; e < R * R; e += 256) {
     const int ry = e / R, rx = e - ry * R;
     const int py = ty0 + ry, px = tx0 + rx;
-    float rec[kMaxC] = {0.f, 0.f, 0.f, 0.f};
+    float rec[kMaxC] = {};
     float m = 0.f;
     const bool in = py < H && px < W;
     if (in) {
@@ -152,7 +163,7 @@ __global__ __launch_bounds__(256) void photo_fwd_kernel(const float* __restrict_
       ssim += fminf(fmaxf((1.f - n / d) / 2.f, 0.f), 1.f);
     }
   }
-  const int blk = blockIdx.y * gridDim.x + blockIdx.x;
+  const int blk = b * gridDim.x + (ty0 / kTile) * tiles_x + tx0 / kTile;  // fixed slot per tile
   block_sum3(l1, ssim, msum, red, partials + 3 * blk);
 }
 
@@ -212,9 +223,10 @@ __global__ __launch_bounds__(256) void photo_bwd_kernel(const float* __restrict_
   constexpr int RW = kTile + 2;  // windows: top-left rows ty0-2 .. ty0+TH-1
   __shared__ float xs[kMaxC][RI][RI + 1], ys[kMaxC][RI][RI + 1];
   __shared__ float al[kMaxC][RW][RW + 1], be[kMaxC][RW][RW + 1], ga[kMaxC][RW][RW + 1];
+  __shared__ float corners[kMaxC][4][kTile * kTile];  // own pixels' source corners
   const int t = threadIdx.x;
-  const int b = blockIdx.y;
-  const int ty0 = (blockIdx.x / tiles_x) * kTile, tx0 = (blockIdx.x % tiles_x) * kTile;
+  int ty0, tx0, b;
+  photo_work(tiles_x, ty0, tx0, b);
   const int HW = H * W;
   const float* srcb = src + (size_t)b * C * HW;
   const float* tgtb = tgt + (size_t)b * C * HW;
@@ -224,19 +236,37 @@ __global__ __launch_bounds__(256) void photo_bwd_kernel(const float* __restrict_
   for (int e = t; e < RI * RI; e += 256) {
     const int ry = e / RI, rx = e - ry * RI;
     const int py = ty0 - 2 + ry, px = tx0 - 2 + rx;
-    float rec[kMaxC] = {0.f, 0.f, 0.f, 0.f};
     float m = 0.f;
     const bool in = py >= 0 && px >= 0 && py < H && px < W;
+    const bool own = ry >= 2 && rx >= 2 && ry < kTile + 2 && rx < kTile + 2;
+    const int o = (ry - 2) * kTile + (rx - 2);
+    Tap tp;
     if (in) {
-      Tap tp;
-      sample_px(srcb, fb, px, py, H, W, C, BORDER, rec, tp);
+      tp = make_tap(fb[py * W + px], fb[HW + py * W + px], px, py, H, W, BORDER);
       m = mb[py * W + px];
     }
+    // one channel at a time: gather the 4 corners, keep them in LDS for the
+    // owned pixels (the coordinate derivative below needs them), store x and y
 #pragma unroll
     for (int c = 0; c < kMaxC; ++c) {
       if (c >= C) break;
-      xs[c][ry][rx] = rec[c] * m;
+      float v0 = 0.f, v1 = 0.f, v2 = 0.f, v3 = 0.f, r = 0.f;
+      if (in) {
+        const float* sc = srcb + (size_t)c * HW;
+        v0 = tp.m_nw ? sc[tp.o_nw] : 0.f;
+        v1 = tp.m_ne ? sc[tp.o_ne] : 0.f;
+        v2 = tp.m_sw ? sc[tp.o_sw] : 0.f;
+        v3 = tp.m_se ? sc[tp.o_se] : 0.f;
+        r = v0 * (tp.s * tp.e) + v1 * (tp.s * tp.w) + v2 * (tp.n * tp.e) + v3 * (tp.n * tp.w);
+      }
+      xs[c][ry][rx] = r * m;
       ys[c][ry][rx] = in ? tgtb[(size_t)c * HW + py * W + px] * m : 0.f;
+      if (own) {
+        corners[c][0][o] = v0;
+        corners[c][1][o] = v1;
+        corners[c][2][o] = v2;
+        corners[c][3][o] = v3;
+      }
     }
   }
   __syncthreads();
@@ -287,10 +317,9 @@ __global__ __launch_bounds__(256) void photo_bwd_kernel(const float* __restrict_
   if (py >= H || px >= W) return;
   const float gl = *gloss;
   const float c_l1 = coef[1] * gl, c_ss = coef[2] * gl;
-  Tap tp;
-  float rec[kMaxC] = {0.f, 0.f, 0.f, 0.f};
-  sample_px(srcb, fb, px, py, H, W, C, BORDER, rec, tp);
-  const float m = mb[py * W + px];
+  const int HWp = py * W + px;
+  const Tap tp = make_tap(fb[HWp], fb[HW + HWp], px, py, H, W, BORDER);  // weights + masks only
+  const float m = mb[HWp];
   float dix = 0.f, diy = 0.f;
 #pragma unroll
   for (int c = 0; c < kMaxC; ++c) {
@@ -307,14 +336,12 @@ __global__ __launch_bounds__(256) void photo_bwd_kernel(const float* __restrict_
       }
     const float xp = xs[c][ly + 2][lx + 2], yp = ys[c][ly + 2][lx + 2];
     const float tv = tgtb[(size_t)c * HW + py * W + px];
-    const float diff = rec[c] - tv;
+    const float vnw = corners[c][0][t], vne = corners[c][1][t];
+    const float vsw = corners[c][2][t], vse = corners[c][3][t];
+    const float rec = vnw * (tp.s * tp.e) + vne * (tp.s * tp.w) + vsw * (tp.n * tp.e) + vse * (tp.n * tp.w);
+    const float diff = rec - tv;
     const float sgn = diff > 0.f ? 1.f : (diff < 0.f ? -1.f : 0.f);
     const float g = (c_l1 * sgn + c_ss * (sa + sb * xp + sg * yp)) * m;  // dL / d rec_c
-    const float* sc = srcb + (size_t)c * HW;
-    const float vnw = tp.m_nw ? sc[tp.o_nw] : 0.f;
-    const float vne = tp.m_ne ? sc[tp.o_ne] : 0.f;
-    const float vsw = tp.m_sw ? sc[tp.o_sw] : 0.f;
-    const float vse = tp.m_se ? sc[tp.o_se] : 0.f;
     dix += ((vne - vnw) * tp.s + (vse - vsw) * tp.n) * g;
     diy += ((vsw - vnw) * tp.e + (vse - vne) * tp.w) * g;
   }

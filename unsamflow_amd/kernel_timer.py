@@ -154,6 +154,25 @@ def site_launcher(op: str, key, device, seed: int = 0):
         need1, need2 = key[4], key[5]
         go = torch.randn(B, 81, H, W, device=device, generator=g)
         return lambda: ops.corr_backward(x1, x2, go, 4, need1, need2)
+    if op in ("occ_bwd", "splat", "photo_fwd", "photo_bwd"):
+        B, C, H, W = key[:4]
+        yy = torch.linspace(0, 6.2832, H, device=device).view(1, 1, H, 1)
+        xx = torch.linspace(0, 6.2832, W, device=device).view(1, 1, 1, W)
+        ph = torch.rand(B, 2, 1, 1, device=device, generator=g) * 6.2832
+        flow = (torch.sin(2 * xx + ph) + torch.cos(3 * yy - ph)).contiguous()
+        if op == "occ_bwd":
+            return lambda: ops.occ_backward(flow, 0.2)
+        if op == "splat":
+            return lambda: ops.splat_map(flow, bool(key[4]))
+        pad = key[4]
+        src = torch.rand(B, C, H, W, device=device, generator=g)
+        tgt = torch.rand(B, C, H, W, device=device, generator=g)
+        mask = (torch.rand(B, 1, H, W, device=device, generator=g) > 0.1).float()
+        if op == "photo_fwd":
+            return lambda: ops.photo_loss_forward(src, tgt, mask, flow, pad)
+        coef = ops.photo_loss_forward(src, tgt, mask, flow, pad)
+        gl = torch.ones(1, device=device)
+        return lambda: ops.photo_loss_backward(src, tgt, mask, flow, coef, gl, pad)
     B, C, H, W, pad = key[:5]
     x = torch.rand(B, C, H, W, device=device, generator=g)
     yy = torch.linspace(0, 6.2832, H, device=device).view(1, 1, H, 1)

@@ -235,8 +235,8 @@ def _photo_args(src, tgt, mask, flow):
     B, C, H, W = _nchw("src", src)
     if tuple(tgt.shape) != (B, C, H, W) or tuple(mask.shape) != (B, 1, H, W):
         raise ValueError(f"tgt {tuple(tgt.shape)} / mask {tuple(mask.shape)} do not match src {(B, C, H, W)}")
-    if C > 4:
-        raise NotImplementedError(f"fused photometric loss supports C <= 4 image channels, got {C}")
+    if C > 3:
+        raise NotImplementedError(f"fused photometric loss supports C <= 3 image channels, got {C}")
     _require_device_f32("flow", flow)
     fv, fbs = _flow_view(flow, B, H, W)
     return src.contiguous(), tgt.contiguous(), mask.contiguous(), fv, fbs, B, C, H, W
