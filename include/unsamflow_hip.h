@@ -12,6 +12,9 @@
  *   usf_corr_bwd_f32  <- correlation_cuda.backward
  *                        (models/correlation_package/correlation_cuda.cc:88-165;
  *                         Python caller correlation.py:40-72)
+ *   usf_corr_{fwd,bwd}_ex_f32 <- the same plus the decoder's LeakyReLU and the
+ *                        concat into the flow-estimator input (pwclite.py:
+ *                        307-308, 364-366)
  *   usf_warp_fwd_f32  <- grid_sample(bilinear, align_corners=True) inside
  *                        flow_warp (utils/warp_utils.py:97-106, incl.
  *                        mesh_grid :7-13 and norm_grid :16-23)
@@ -82,6 +85,29 @@ int usf_corr_fwd_f32(const float* x1, const float* x2, float* out,
 int usf_corr_bwd_f32(const float* x1, const float* x2, const float* gout,
                      float* gx1, float* gx2,
                      int B, int C, int H, int W, int d, void* stream);
+
+/* Activations of the fused correlation epilogue (the decoder's in-place
+ * nn.LeakyReLU(0.1) right after every correlation, pwclite.py:307-308). */
+#define USF_ACT_NONE 0
+#define USF_ACT_LEAKY_RELU 1
+
+/* usf_corr_fwd_f32 writing into a channel slice of a larger buffer (the flow
+ * estimator's concat input, pwclite.py:364-366): sample b's (2d+1)^2 output
+ * planes start at out + b * out_bstride (elements; planes H*W apart), and
+ * act = USF_ACT_LEAKY_RELU applies v > 0 ? v : v * slope to every output. */
+int usf_corr_fwd_ex_f32(const float* x1, const float* x2, float* out, long long out_bstride,
+                        int act, float slope, int B, int C, int H, int W, int d,
+                        void* stream);
+
+/* usf_corr_bwd_f32 reading its gradient from a channel slice (batch stride
+ * g_bstride, elements). With act_out != NULL (the forward's activated output,
+ * same layout as gout) the LeakyReLU derivative g * (act_out > 0 ? 1 : slope)
+ * is applied first -- torch's leaky_relu_backward on the result, as for the
+ * in-place module -- in one dense pass into `scratch` (caller-provided,
+ * B*(2d+1)^2*H*W floats; unused when act_out is NULL). */
+int usf_corr_bwd_ex_f32(const float* x1, const float* x2, const float* gout, long long g_bstride,
+                        const float* act_out, float slope, float* scratch, float* gx1, float* gx2,
+                        int B, int C, int H, int W, int d, void* stream);
 
 /* Bilinear backward warp (flow_warp), align_corners=True.
  * x: [B,C,H,W]; flow: [B,2,H,W] with batch stride flow_bstride (elements);

@@ -34,6 +34,15 @@ _SIGNATURES = {
         [_c_float_p] * 5 + [ctypes.c_int] * 5 + [ctypes.c_void_p],
         ctypes.c_int,
     ),
+    "usf_corr_fwd_ex_f32": (
+        [_c_float_p] * 3 + [ctypes.c_longlong, ctypes.c_int, ctypes.c_float] + [ctypes.c_int] * 5 + [ctypes.c_void_p],
+        ctypes.c_int,
+    ),
+    "usf_corr_bwd_ex_f32": (
+        [_c_float_p] * 3 + [ctypes.c_longlong, _c_float_p, ctypes.c_float] + [_c_float_p] * 3
+        + [ctypes.c_int] * 5 + [ctypes.c_void_p],
+        ctypes.c_int,
+    ),
     "usf_warp_fwd_f32": (
         [_c_float_p, _c_float_p, ctypes.c_longlong, _c_float_p] + [ctypes.c_int] * 5 + [ctypes.c_void_p],
         ctypes.c_int,

@@ -97,8 +97,39 @@ int usf_corr_fwd_f32(const float* x1, const float* x2, float* out, int B, int C,
     return USF_EINVAL;
   }
   if (const int pe = pre_check("usf_corr_fwd_f32", (hipStream_t)stream)) return pe;
+  const long long k2 = (long long)(2 * d + 1) * (2 * d + 1);
   return finish("usf_corr_fwd_f32",
-                corr_fwd_launch(x1, x2, out, B, C, H, W, d, (hipStream_t)stream), (hipStream_t)stream);
+                corr_fwd_launch(x1, x2, out, B, C, H, W, d, (hipStream_t)stream,
+                                FwdEpi{k2 * H * W, 0, 0.f}),
+                (hipStream_t)stream);
+}
+
+int usf_corr_fwd_ex_f32(const float* x1, const float* x2, float* out, long long out_bstride,
+                        int act, float slope, int B, int C, int H, int W, int d, void* stream) {
+  clear_error();
+  if (!check_dims("usf_corr_fwd_ex_f32", B, C, H, W)) return USF_EINVAL;
+  if (d < 1 || d > 4) {
+    set_error("usf_corr_fwd_ex_f32: max_displacement %d not in [1,4]", d);
+    return USF_EINVAL;
+  }
+  if (!x1 || !x2 || !out) {
+    set_error("usf_corr_fwd_ex_f32: null pointer");
+    return USF_EINVAL;
+  }
+  const long long k2 = (long long)(2 * d + 1) * (2 * d + 1);
+  if (out_bstride < k2 * H * W && B > 1) {
+    set_error("usf_corr_fwd_ex_f32: out batch stride %lld < (2d+1)^2*H*W", out_bstride);
+    return USF_EINVAL;
+  }
+  if (act != USF_ACT_NONE && act != USF_ACT_LEAKY_RELU) {
+    set_error("usf_corr_fwd_ex_f32: unknown act %d", act);
+    return USF_EINVAL;
+  }
+  if (const int pe = pre_check("usf_corr_fwd_ex_f32", (hipStream_t)stream)) return pe;
+  return finish("usf_corr_fwd_ex_f32",
+                corr_fwd_launch(x1, x2, out, B, C, H, W, d, (hipStream_t)stream,
+                                FwdEpi{out_bstride, act, slope}),
+                (hipStream_t)stream);
 }
 
 int usf_corr_bwd_f32(const float* x1, const float* x2, const float* gout, float* gx1,
@@ -114,8 +145,47 @@ int usf_corr_bwd_f32(const float* x1, const float* x2, const float* gout, float*
     return USF_EINVAL;
   }
   if (const int pe = pre_check("usf_corr_bwd_f32", (hipStream_t)stream)) return pe;
+  const long long k2 = (long long)(2 * d + 1) * (2 * d + 1);
   return finish("usf_corr_bwd_f32",
-                corr_bwd_launch(x1, x2, gout, gx1, gx2, B, C, H, W, d, (hipStream_t)stream),
+                corr_bwd_launch(x1, x2, gout, gx1, gx2, B, C, H, W, d, (hipStream_t)stream,
+                                BwdEpi{k2 * H * W}),
+                (hipStream_t)stream);
+}
+
+int usf_corr_bwd_ex_f32(const float* x1, const float* x2, const float* gout, long long g_bstride,
+                        const float* act_out, float slope, float* scratch, float* gx1, float* gx2,
+                        int B, int C, int H, int W, int d, void* stream) {
+  clear_error();
+  if (!check_dims("usf_corr_bwd_ex_f32", B, C, H, W)) return USF_EINVAL;
+  if (d < 1 || d > 4) {
+    set_error("usf_corr_bwd_ex_f32: max_displacement %d not in [1,4]", d);
+    return USF_EINVAL;
+  }
+  if (!gout || (gx1 && !x2) || (gx2 && !x1)) {
+    set_error("usf_corr_bwd_ex_f32: null input pointer");
+    return USF_EINVAL;
+  }
+  const long long k2 = (long long)(2 * d + 1) * (2 * d + 1);
+  if (g_bstride < k2 * H * W && B > 1) {
+    set_error("usf_corr_bwd_ex_f32: gradient batch stride %lld < (2d+1)^2*H*W", g_bstride);
+    return USF_EINVAL;
+  }
+  if (act_out && !scratch) {
+    set_error("usf_corr_bwd_ex_f32: act_out needs a scratch of B*(2d+1)^2*H*W floats");
+    return USF_EINVAL;
+  }
+  if (const int pe = pre_check("usf_corr_bwd_ex_f32", (hipStream_t)stream)) return pe;
+  const float* g = gout;
+  long long gbs = g_bstride;
+  if (act_out) {  // LeakyReLU derivative + de-concat in one dense pass, then the plain backward
+    const hipError_t e = leaky_bwd_gather_launch(gout, act_out, g_bstride, slope, scratch, B,
+                                                 (int)k2, H, W, (hipStream_t)stream);
+    if (e != hipSuccess) return finish("usf_corr_bwd_ex_f32", e, (hipStream_t)stream);
+    g = scratch;
+    gbs = k2 * H * W;
+  }
+  return finish("usf_corr_bwd_ex_f32",
+                corr_bwd_launch(x1, x2, g, gx1, gx2, B, C, H, W, d, (hipStream_t)stream, BwdEpi{gbs}),
                 (hipStream_t)stream);
 }
 

@@ -277,7 +277,7 @@ template <int D, int PX, int SEGX, int NDY, int CC, int V>
 __global__ __launch_bounds__(64 * NDY) void corr_fwd_kernel(const float* __restrict__ x1,
                                                             const float* __restrict__ x2,
                                                             float* __restrict__ out, int C,
-                                                            int H, int W, int tiles_x) {
+                                                            int H, int W, int tiles_x, FwdEpi ep) {
   using F = FwdCfg<D, PX, SEGX, NDY, CC, V>;
   constexpr int K = F::K, TW = F::TW, TH = F::TH, S = F::S;
   constexpr int P1 = F::X1::PL, P2 = F::X2::PL, N1 = F::X1::N;
@@ -359,60 +359,67 @@ __global__ __launch_bounds__(64 * NDY) void corr_fwd_kernel(const float* __restr
   if (y >= H) return;
   const int xb = x0 + q * PX;
   const float cf = (float)C;
-  float* ob = out + ((size_t)b * K * K + (size_t)dy * K) * HW + y * W + xb;
-  const bool vec = ((W & 3) == 0) && (xb + PX <= W);
+  // output planes of sample b start at b * ep.out_bstride (a channel slice of a
+  // concat buffer, or the dense [B,K*K,H,W] tensor); LeakyReLU epilogue on request
+  float* ob = out + (size_t)b * ep.out_bstride + (size_t)dy * K * HW + y * W + xb;
+  const bool leaky = ep.act != 0;
+  const float slope = ep.slope;
+  auto epi = [&](float a) {
+    const float v = a / cf;
+    return leaky ? (v > 0.f ? v : v * slope) : v;
+  };
+  const bool vec = ((W & 3) == 0) && ((ep.out_bstride & 3) == 0) && (xb + PX <= W);
 #pragma unroll
   for (int dx = 0; dx < K; ++dx) {
     float* o = ob + dx * HW;
     if (vec) {
 #pragma unroll
       for (int i = 0; i < PX / 4; ++i)
-        reinterpret_cast<float4*>(o)[i] =
-            make_float4(acc[dx][4 * i] / cf, acc[dx][4 * i + 1] / cf, acc[dx][4 * i + 2] / cf,
-                        acc[dx][4 * i + 3] / cf);
+        reinterpret_cast<float4*>(o)[i] = make_float4(epi(acc[dx][4 * i]), epi(acc[dx][4 * i + 1]),
+                                                      epi(acc[dx][4 * i + 2]), epi(acc[dx][4 * i + 3]));
     } else {
 #pragma unroll
       for (int i = 0; i < PX; ++i)
-        if (xb + i < W) o[i] = acc[dx][i] / cf;
+        if (xb + i < W) o[i] = epi(acc[dx][i]);
     }
   }
 }
 
 template <int D, int PX, int SEGX, int NDY, int CC, int V>
 hipError_t launch_fwd_v(const float* x1, const float* x2, float* out, int B, int C, int H, int W,
-                        hipStream_t s) {
+                        hipStream_t s, FwdEpi ep) {
   using F = FwdCfg<D, PX, SEGX, NDY, CC, V>;
   const int tiles_x = (W + F::TW - 1) / F::TW;
   const int tiles_y = (H + F::TH - 1) / F::TH;
   dim3 grid(F::NDYG, tiles_x * tiles_y, B);
   hipLaunchKernelGGL((corr_fwd_kernel<D, PX, SEGX, NDY, CC, V>), grid, dim3(F::NT), 0, s, x1,
-                     x2, out, C, H, W, tiles_x);
+                     x2, out, C, H, W, tiles_x, ep);
   return hipGetLastError();
 }
 
 // 16-byte DMA staging whenever the layout and W allow it (see Layout).
 template <int D, int PX, int SEGX, int NDY, int CC>
 hipError_t launch_fwd(const float* x1, const float* x2, float* out, int B, int C, int H, int W,
-                      hipStream_t s) {
+                      hipStream_t s, FwdEpi ep) {
   if constexpr (Layout<PX, SEGX, D>::X4) {
-    if (W % 4 == 0) return launch_fwd_v<D, PX, SEGX, NDY, CC, 4>(x1, x2, out, B, C, H, W, s);
+    if (W % 4 == 0) return launch_fwd_v<D, PX, SEGX, NDY, CC, 4>(x1, x2, out, B, C, H, W, s, ep);
   }
-  return launch_fwd_v<D, PX, SEGX, NDY, CC, 1>(x1, x2, out, B, C, H, W, s);
+  return launch_fwd_v<D, PX, SEGX, NDY, CC, 1>(x1, x2, out, B, C, H, W, s, ep);
 }
 
 // Tuning hook: usf_set_variant(0, i) forces candidate i for d=4
 // (tools/kbench.py sweeps them on the GPU); -1 = the shape heuristic below.
 hipError_t fwd_candidate_d4(int i, const float* x1, const float* x2, float* out, int B, int C,
-                            int H, int W, hipStream_t s) {
+                            int H, int W, hipStream_t s, FwdEpi ep) {
   switch (i) {
-    case 0: return launch_fwd<4, 8, 8, 9, 8>(x1, x2, out, B, C, H, W, s);
-    case 1: return launch_fwd<4, 8, 8, 9, 4>(x1, x2, out, B, C, H, W, s);
-    case 2: return launch_fwd<4, 4, 8, 9, 8>(x1, x2, out, B, C, H, W, s);
-    case 3: return launch_fwd<4, 4, 8, 9, 4>(x1, x2, out, B, C, H, W, s);
-    case 4: return launch_fwd<4, 4, 8, 3, 8>(x1, x2, out, B, C, H, W, s);
-    case 5: return launch_fwd<4, 4, 8, 3, 4>(x1, x2, out, B, C, H, W, s);
-    case 6: return launch_fwd<4, 8, 8, 3, 4>(x1, x2, out, B, C, H, W, s);
-    case 7: return launch_fwd<4, 4, 8, 1, 8>(x1, x2, out, B, C, H, W, s);
+    case 0: return launch_fwd<4, 8, 8, 9, 8>(x1, x2, out, B, C, H, W, s, ep);
+    case 1: return launch_fwd<4, 8, 8, 9, 4>(x1, x2, out, B, C, H, W, s, ep);
+    case 2: return launch_fwd<4, 4, 8, 9, 8>(x1, x2, out, B, C, H, W, s, ep);
+    case 3: return launch_fwd<4, 4, 8, 9, 4>(x1, x2, out, B, C, H, W, s, ep);
+    case 4: return launch_fwd<4, 4, 8, 3, 8>(x1, x2, out, B, C, H, W, s, ep);
+    case 5: return launch_fwd<4, 4, 8, 3, 4>(x1, x2, out, B, C, H, W, s, ep);
+    case 6: return launch_fwd<4, 8, 8, 3, 4>(x1, x2, out, B, C, H, W, s, ep);
+    case 7: return launch_fwd<4, 4, 8, 1, 8>(x1, x2, out, B, C, H, W, s, ep);
     default: return hipErrorInvalidValue;
   }
 }
@@ -420,21 +427,21 @@ constexpr int kFwdCandidates = 8;
 
 template <int D>
 hipError_t fwd_dispatch(const float* x1, const float* x2, float* out, int B, int C, int H,
-                        int W, hipStream_t s) {
+                        int W, hipStream_t s, FwdEpi ep) {
   constexpr int K = 2 * D + 1;
   if (D == 4) {
     const int forced = variant_override(0);
-    if (forced >= 0) return fwd_candidate_d4(forced, x1, x2, out, B, C, H, W, s);
+    if (forced >= 0) return fwd_candidate_d4(forced, x1, x2, out, B, C, H, W, s, ep);
   }
   // All displacement rows in one workgroup (x1/x2 staged once) when that
   // still fills the 256 CUs; else split displacement rows across workgroups.
   // (profiles/r01_v4_kbench.json: <4,8,9,4> is the fastest d=4 candidate at
   // the 64x208 level, <4,8,3,8> at 32x104 and below.)
   const long big = (long)B * ((W + 63) / 64) * ((H + 7) / 8);
-  if (big >= 256) return launch_fwd<D, 4, 8, K, 4>(x1, x2, out, B, C, H, W, s);
+  if (big >= 256) return launch_fwd<D, 4, 8, K, 4>(x1, x2, out, B, C, H, W, s, ep);
   const long mid = (long)B * ((W + 31) / 32) * ((H + 7) / 8);
-  if (mid >= 256) return launch_fwd<D, 4, 8, K, 8>(x1, x2, out, B, C, H, W, s);
-  return launch_fwd<D, 4, 8, 3, 8>(x1, x2, out, B, C, H, W, s);
+  if (mid >= 256) return launch_fwd<D, 4, 8, K, 8>(x1, x2, out, B, C, H, W, s, ep);
+  return launch_fwd<D, 4, 8, 3, 8>(x1, x2, out, B, C, H, W, s, ep);
 }
 
 // --------------------------------------------------------------- backward --
@@ -466,7 +473,8 @@ template <int D, int PX, int SEGX, int NW, int CC, int V, bool G2>
 __device__ __forceinline__ void corr_bwd_tile(float* sm, const float* __restrict__ xs,
                                               const float* __restrict__ g,
                                               float* __restrict__ gx, int tile, int group, int b,
-                                              int C, int H, int W, int tiles_x, int cg) {
+                                              int C, int H, int W, int tiles_x, int cg,
+                                              const BwdEpi& ep) {
   using F = BwdCfg<D, PX, SEGX, NW, CC, V>;
   constexpr int K = F::K, TW = F::TW, TH = F::TH, NT = F::NT, S = F::S, P = F::P;
   constexpr int WIN = F::WIN, DYW = F::DYW, XIMG = F::XIMG;
@@ -487,7 +495,9 @@ __device__ __forceinline__ void corr_bwd_tile(float* sm, const float* __restrict
 
   const int HW = H * W;
   const float* xsb = xs + (size_t)b * C * HW;
-  const float* gb = g + (size_t)b * K * K * HW;
+  // g of sample b at b * ep.g_bstride: a channel slice of the concat gradient,
+  // or the dense [B,K*K,H,W] tensor
+  const float* gb = g + (size_t)b * ep.g_bstride;
 
   // this wave's DYW rows of g for its PX pixels, read once (clamped unconditional loads)
   float gv[DYW][K][PX];
@@ -599,16 +609,17 @@ __device__ __forceinline__ void corr_bwd_tile(float* sm, const float* __restrict
 // 40 KB LDS, i.e. 3 waves/SIMD = 4 resident workgroups of 3 waves per CU.
 // amdgpu_waves_per_eu(3) pins the VGPR target: without it, allocation for the
 // two inlined direction bodies flips between 163 and 231 on unrelated edits.
-template <int D, int PX, int SEGX, int NW, int CC, int V, int MODE>
 #ifndef USF_BWD_WAVES_PER_EU
 #define USF_BWD_WAVES_PER_EU 3
 #endif
+template <int D, int PX, int SEGX, int NW, int CC, int V, int MODE>
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(USF_BWD_WAVES_PER_EU))) void corr_bwd_kernel(const float* __restrict__ x1,
                                                            const float* __restrict__ x2,
                                                            const float* __restrict__ g,
                                                            float* __restrict__ gx1,
                                                            float* __restrict__ gx2, int B, int C,
-                                                           int H, int W, int tiles_x, int cg) {
+                                                           int H, int W, int tiles_x, int cg,
+                                                           BwdEpi ep) {
   __shared__ __attribute__((aligned(16))) float sm[BwdCfg<D, PX, SEGX, NW, CC, V>::LDSN];
   USF_TRACE_AT(0);
   USF_TRACE_HWID();
@@ -621,16 +632,16 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(USF_BWD
   const int tile = (w / gridDim.y) % gridDim.x;
   int b = w / (gridDim.x * gridDim.y);
   if constexpr (MODE == 1) {
-    corr_bwd_tile<D, PX, SEGX, NW, CC, V, false>(sm, x2, g, gx1, tile, group, b, C, H, W, tiles_x, cg);
+    corr_bwd_tile<D, PX, SEGX, NW, CC, V, false>(sm, x2, g, gx1, tile, group, b, C, H, W, tiles_x, cg, ep);
   } else if constexpr (MODE == 2) {
-    corr_bwd_tile<D, PX, SEGX, NW, CC, V, true>(sm, x1, g, gx2, tile, group, b, C, H, W, tiles_x, cg);
+    corr_bwd_tile<D, PX, SEGX, NW, CC, V, true>(sm, x1, g, gx2, tile, group, b, C, H, W, tiles_x, cg, ep);
   } else {
     if (b >= B)
       corr_bwd_tile<D, PX, SEGX, NW, CC, V, true>(sm, x1, g, gx2, tile, group, b - B, C, H, W,
-                                                  tiles_x, cg);
+                                                  tiles_x, cg, ep);
     else
       corr_bwd_tile<D, PX, SEGX, NW, CC, V, false>(sm, x2, g, gx1, tile, group, b, C, H, W,
-                                                   tiles_x, cg);
+                                                   tiles_x, cg, ep);
   }
 }
 
@@ -641,7 +652,7 @@ constexpr int kBwdTargetWorkgroups = 768;
 
 template <int D, int PX, int SEGX, int NW, int CC, int V, int MODE>
 hipError_t launch_bwd_mode(const float* x1, const float* x2, const float* g, float* gx1,
-                           float* gx2, int B, int C, int H, int W, hipStream_t s) {
+                           float* gx2, int B, int C, int H, int W, hipStream_t s, BwdEpi ep) {
   using F = BwdCfg<D, PX, SEGX, NW, CC, V>;
   const int dirs = MODE == 3 ? 2 : 1;
   const int tiles_x = (W + F::TW - 1) / F::TW;
@@ -652,39 +663,39 @@ hipError_t launch_bwd_mode(const float* x1, const float* x2, const float* g, flo
   const int cg = round_up((C + groups - 1) / groups, CC);
   dim3 grid(tiles_x * tiles_y, (C + cg - 1) / cg, B * dirs);
   hipLaunchKernelGGL((corr_bwd_kernel<D, PX, SEGX, NW, CC, V, MODE>), grid, dim3(F::NT), 0, s, x1,
-                     x2, g, gx1, gx2, B, C, H, W, tiles_x, cg);
+                     x2, g, gx1, gx2, B, C, H, W, tiles_x, cg, ep);
   return hipGetLastError();
 }
 
 template <int D, int PX, int SEGX, int NW, int CC, int V>
 hipError_t launch_bwd_v(const float* x1, const float* x2, const float* g, float* gx1, float* gx2,
-                        int B, int C, int H, int W, hipStream_t s) {
+                        int B, int C, int H, int W, hipStream_t s, BwdEpi ep) {
   if (gx1 && gx2)
-    return launch_bwd_mode<D, PX, SEGX, NW, CC, V, 3>(x1, x2, g, gx1, gx2, B, C, H, W, s);
+    return launch_bwd_mode<D, PX, SEGX, NW, CC, V, 3>(x1, x2, g, gx1, gx2, B, C, H, W, s, ep);
   hipError_t e = hipSuccess;
-  if (gx1) e = launch_bwd_mode<D, PX, SEGX, NW, CC, V, 1>(x1, x2, g, gx1, gx2, B, C, H, W, s);
+  if (gx1) e = launch_bwd_mode<D, PX, SEGX, NW, CC, V, 1>(x1, x2, g, gx1, gx2, B, C, H, W, s, ep);
   if (e == hipSuccess && gx2)
-    e = launch_bwd_mode<D, PX, SEGX, NW, CC, V, 2>(x1, x2, g, gx1, gx2, B, C, H, W, s);
+    e = launch_bwd_mode<D, PX, SEGX, NW, CC, V, 2>(x1, x2, g, gx1, gx2, B, C, H, W, s, ep);
   return e;
 }
 
 template <int D, int PX = 4, int SEGX = 8, int NW = 3, int CC = 4>
 hipError_t launch_bwd(const float* x1, const float* x2, const float* g, float* gx1, float* gx2,
-                      int B, int C, int H, int W, hipStream_t s) {
+                      int B, int C, int H, int W, hipStream_t s, BwdEpi ep) {
   if constexpr (Layout<PX, SEGX, D>::X4) {
     if (W % 4 == 0)
-      return launch_bwd_v<D, PX, SEGX, NW, CC, 4>(x1, x2, g, gx1, gx2, B, C, H, W, s);
+      return launch_bwd_v<D, PX, SEGX, NW, CC, 4>(x1, x2, g, gx1, gx2, B, C, H, W, s, ep);
   }
-  return launch_bwd_v<D, PX, SEGX, NW, CC, 1>(x1, x2, g, gx1, gx2, B, C, H, W, s);
+  return launch_bwd_v<D, PX, SEGX, NW, CC, 1>(x1, x2, g, gx1, gx2, B, C, H, W, s, ep);
 }
 
 hipError_t bwd_candidate_d4(int i, const float* x1, const float* x2, const float* g, float* gx1,
-                            float* gx2, int B, int C, int H, int W, hipStream_t s) {
+                            float* gx2, int B, int C, int H, int W, hipStream_t s, BwdEpi ep) {
   switch (i) {
-    case 0: return launch_bwd<4, 4, 8, 3, 4>(x1, x2, g, gx1, gx2, B, C, H, W, s);
-    case 1: return launch_bwd<4, 4, 8, 3, 8>(x1, x2, g, gx1, gx2, B, C, H, W, s);
-    case 2: return launch_bwd<4, 4, 8, 9, 4>(x1, x2, g, gx1, gx2, B, C, H, W, s);
-    case 3: return launch_bwd<4, 4, 8, 9, 8>(x1, x2, g, gx1, gx2, B, C, H, W, s);
+    case 0: return launch_bwd<4, 4, 8, 3, 4>(x1, x2, g, gx1, gx2, B, C, H, W, s, ep);
+    case 1: return launch_bwd<4, 4, 8, 3, 8>(x1, x2, g, gx1, gx2, B, C, H, W, s, ep);
+    case 2: return launch_bwd<4, 4, 8, 9, 4>(x1, x2, g, gx1, gx2, B, C, H, W, s, ep);
+    case 3: return launch_bwd<4, 4, 8, 9, 8>(x1, x2, g, gx1, gx2, B, C, H, W, s, ep);
     default: return hipErrorInvalidValue;
   }
 }
@@ -692,14 +703,52 @@ constexpr int kBwdCandidates = 4;
 
 template <int D>
 hipError_t bwd_dispatch(const float* x1, const float* x2, const float* g, float* gx1, float* gx2,
-                        int B, int C, int H, int W, hipStream_t s) {
+                        int B, int C, int H, int W, hipStream_t s, BwdEpi ep) {
   if (D == 4) {
     const int forced = variant_override(1);
-    if (forced >= 0) return bwd_candidate_d4(forced, x1, x2, g, gx1, gx2, B, C, H, W, s);
+    if (forced >= 0) return bwd_candidate_d4(forced, x1, x2, g, gx1, gx2, B, C, H, W, s, ep);
   }
-  return launch_bwd<D>(x1, x2, g, gx1, gx2, B, C, H, W, s);
+  return launch_bwd<D>(x1, x2, g, gx1, gx2, B, C, H, W, s, ep);
 }
 
+// g_eff[b, k, p] = g[b * g_bstride + k * HW + p] * (act[...] > 0 ? 1 : slope):
+// torch's leaky_relu_backward on the result (the in-place module's form), read
+// from the concat-gradient slice and written dense for the backward kernel.
+__global__ __launch_bounds__(256) void leaky_bwd_gather_kernel(const float* __restrict__ g,
+                                                               const float* __restrict__ act,
+                                                               long long gbs, float slope,
+                                                               float* __restrict__ out, int K2,
+                                                               int HW) {
+  const long long per = (long long)K2 * HW;
+  const long long i = ((long long)blockIdx.x * 256 + threadIdx.x) * 4;
+  const int b = blockIdx.y;
+  if (i >= per) return;
+  const float* gb = g + (size_t)b * gbs;
+  const float* ab = act + (size_t)b * gbs;
+  float* ob = out + (size_t)b * per;
+  if (i + 3 < per && (gbs & 3) == 0) {
+    const float4 gv = *reinterpret_cast<const float4*>(gb + i);
+    const float4 av = *reinterpret_cast<const float4*>(ab + i);
+    *reinterpret_cast<float4*>(ob + i) =
+        make_float4(av.x > 0.f ? gv.x : gv.x * slope, av.y > 0.f ? gv.y : gv.y * slope,
+                    av.z > 0.f ? gv.z : gv.z * slope, av.w > 0.f ? gv.w : gv.w * slope);
+  } else {
+    for (long long j = i; j < per && j < i + 4; ++j) ob[j] = ab[j] > 0.f ? gb[j] : gb[j] * slope;
+  }
+}
+
+}  // namespace
+
+hipError_t leaky_bwd_gather_launch(const float* g, const float* act, long long g_bstride, float slope,
+                                   float* out, int B, int K2, int H, int W, hipStream_t s) {
+  const long long per = (long long)K2 * H * W;
+  const dim3 grid((unsigned)((per + 1023) / 1024), (unsigned)B);
+  hipLaunchKernelGGL(leaky_bwd_gather_kernel, grid, dim3(256), 0, s, g, act, g_bstride, slope, out,
+                     K2, H * W);
+  return hipGetLastError();
+}
+
+namespace {
 }  // namespace
 
 static int g_variant[3] = {-1, -1, -1};
@@ -708,23 +757,23 @@ int variant_count(int op) { return op == 0 ? kFwdCandidates : op == 1 ? kBwdCand
 void set_variant_override(int op, int index) { __atomic_store_n(&g_variant[op], index, __ATOMIC_RELAXED); }
 
 hipError_t corr_fwd_launch(const float* x1, const float* x2, float* out, int B, int C, int H,
-                           int W, int d, hipStream_t s) {
+                           int W, int d, hipStream_t s, FwdEpi ep) {
   switch (d) {
-    case 1: return fwd_dispatch<1>(x1, x2, out, B, C, H, W, s);
-    case 2: return fwd_dispatch<2>(x1, x2, out, B, C, H, W, s);
-    case 3: return fwd_dispatch<3>(x1, x2, out, B, C, H, W, s);
-    case 4: return fwd_dispatch<4>(x1, x2, out, B, C, H, W, s);
+    case 1: return fwd_dispatch<1>(x1, x2, out, B, C, H, W, s, ep);
+    case 2: return fwd_dispatch<2>(x1, x2, out, B, C, H, W, s, ep);
+    case 3: return fwd_dispatch<3>(x1, x2, out, B, C, H, W, s, ep);
+    case 4: return fwd_dispatch<4>(x1, x2, out, B, C, H, W, s, ep);
     default: return hipErrorInvalidValue;
   }
 }
 
 hipError_t corr_bwd_launch(const float* x1, const float* x2, const float* gout, float* gx1,
-                           float* gx2, int B, int C, int H, int W, int d, hipStream_t s) {
+                           float* gx2, int B, int C, int H, int W, int d, hipStream_t s, BwdEpi ep) {
   switch (d) {
-    case 1: return bwd_dispatch<1>(x1, x2, gout, gx1, gx2, B, C, H, W, s);
-    case 2: return bwd_dispatch<2>(x1, x2, gout, gx1, gx2, B, C, H, W, s);
-    case 3: return bwd_dispatch<3>(x1, x2, gout, gx1, gx2, B, C, H, W, s);
-    case 4: return bwd_dispatch<4>(x1, x2, gout, gx1, gx2, B, C, H, W, s);
+    case 1: return bwd_dispatch<1>(x1, x2, gout, gx1, gx2, B, C, H, W, s, ep);
+    case 2: return bwd_dispatch<2>(x1, x2, gout, gx1, gx2, B, C, H, W, s, ep);
+    case 3: return bwd_dispatch<3>(x1, x2, gout, gx1, gx2, B, C, H, W, s, ep);
+    case 4: return bwd_dispatch<4>(x1, x2, gout, gx1, gx2, B, C, H, W, s, ep);
     default: return hipErrorInvalidValue;
   }
 }

@@ -43,11 +43,24 @@ __device__ __forceinline__ int linear_block() {
 // Launchers implemented in corr.hip / warp.hip. They assume validated
 // arguments (capi.cpp checks shapes, d and pointers) and return the
 // hipError_t of the launch.
+// Correlation epilogues: output / gradient batch strides (elements; a channel
+// slice of a concat buffer) and an optional LeakyReLU (act = 1, slope).
+struct FwdEpi {
+  long long out_bstride;
+  int act;
+  float slope;
+};
+struct BwdEpi {
+  long long g_bstride;
+};
+hipError_t leaky_bwd_gather_launch(const float* g, const float* act, long long g_bstride,
+                                   float slope, float* out, int B, int K2, int H, int W,
+                                   hipStream_t s);
 hipError_t corr_fwd_launch(const float* x1, const float* x2, float* out, int B, int C,
-                           int H, int W, int d, hipStream_t s);
+                           int H, int W, int d, hipStream_t s, FwdEpi ep);
 hipError_t corr_bwd_launch(const float* x1, const float* x2, const float* gout,
                            float* gx1, float* gx2, int B, int C, int H, int W, int d,
-                           hipStream_t s);
+                           hipStream_t s, BwdEpi ep);
 hipError_t warp_fwd_launch(const float* x, const float* flow, long long flow_bstride,
                            float* out, int B, int C, int H, int W, int pad_mode,
                            hipStream_t s);

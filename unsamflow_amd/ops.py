@@ -274,3 +274,77 @@ def photo_loss_backward(src, tgt, mask, flow, coef, grad_loss, pad: str = "borde
                                         PAD_MODES[pad], _lib.stream_handle(src.device))
     _lib.check(rc, "usf_photo_loss_bwd_f32")
     return gflow
+
+
+def _plane_slice_stride(name: str, t: torch.Tensor, shape) -> int:
+    """Batch stride of a [B,K,H,W] channel slice whose per-sample planes are dense."""
+    B, K, H, W = shape
+    if tuple(t.shape) != tuple(shape):
+        raise ValueError(f"{name} shape {tuple(t.shape)} != {tuple(shape)}")
+    s = t.stride()
+    if s[1] != H * W or s[2] != W or s[3] != 1 or (B > 1 and s[0] < K * H * W):
+        raise ValueError(f"{name} must be a channel slice of an NCHW-contiguous tensor (strides {s})")
+    return s[0] if B > 1 else K * H * W
+
+
+def corr_forward_ex(x1: torch.Tensor, x2: torch.Tensor, max_displacement: int, out: torch.Tensor,
+                    leaky_slope: float | None = None) -> torch.Tensor:
+    """:func:`corr_forward` into ``out``, a [B,(2d+1)^2,H,W] channel slice of a
+    larger NCHW buffer (the flow estimator's concat input), with the decoder's
+    LeakyReLU applied in the kernel epilogue when ``leaky_slope`` is given."""
+    _require_device_f32("input1", x1)
+    _require_device_f32("input2", x2)
+    _require_device_f32("output", out)
+    B, C, H, W = _nchw("input1", x1)
+    if x2.shape != x1.shape:
+        raise ValueError(f"input2 shape {tuple(x2.shape)} != input1 shape {tuple(x1.shape)}")
+    d = int(max_displacement)
+    K = 2 * d + 1
+    obs = _plane_slice_stride("output", out, (B, K * K, H, W))
+    x1c, x2c = x1.contiguous(), x2.contiguous()
+    lib = _lib.load()
+    act = 0 if leaky_slope is None else 1
+    with torch.cuda.device(x1.device), _kt.timed(
+        "corr_fwd", (B, C, H, W), x1.device, _kt.corr_bytes(B, C, H, W, K * K), _kt.corr_flops(B, C, H, W, K * K)
+    ):
+        rc = lib.usf_corr_fwd_ex_f32(x1c.data_ptr(), x2c.data_ptr(), out.data_ptr(), obs, act,
+                                     float(leaky_slope or 0.0), B, C, H, W, d, _lib.stream_handle(x1.device))
+    _lib.check(rc, "usf_corr_fwd_ex_f32")
+    return out
+
+
+def corr_backward_ex(x1: torch.Tensor, x2: torch.Tensor, grad_out: torch.Tensor, max_displacement: int,
+                     need_x1: bool = True, need_x2: bool = True, act_out: torch.Tensor | None = None,
+                     leaky_slope: float = 0.1) -> tuple[torch.Tensor | None, torch.Tensor | None]:
+    """:func:`corr_backward` reading ``grad_out`` as a channel slice of the concat
+    gradient; with ``act_out`` (the forward's activated slice) the LeakyReLU
+    derivative is applied first (one dense pass into a scratch)."""
+    _require_device_f32("input1", x1)
+    _require_device_f32("input2", x2)
+    _require_device_f32("grad_output", grad_out)
+    B, C, H, W = _nchw("input1", x1)
+    d = int(max_displacement)
+    K = 2 * d + 1
+    gbs = _plane_slice_stride("grad_output", grad_out, (B, K * K, H, W))
+    scratch = None
+    if act_out is not None:
+        _require_device_f32("act_out", act_out)
+        if _plane_slice_stride("act_out", act_out, (B, K * K, H, W)) != gbs:
+            raise ValueError("act_out and grad_output must share the batch stride")
+        scratch = torch.empty((B, K * K, H, W), device=x1.device, dtype=torch.float32)
+    if not (need_x1 or need_x2):
+        return None, None
+    x1c, x2c = x1.contiguous(), x2.contiguous()
+    g1 = torch.empty_like(x1c) if need_x1 else None
+    g2 = torch.empty_like(x2c) if need_x2 else None
+    lib = _lib.load()
+    with torch.cuda.device(x1.device), _kt.timed(
+        "corr_bwd", (B, C, H, W, need_x1, need_x2), x1.device,
+        _kt.corr_bytes(B, C, H, W, K * K, True, need_x1, need_x2),
+        _kt.corr_flops(B, C, H, W, K * K, True, need_x1, need_x2),
+    ):
+        rc = lib.usf_corr_bwd_ex_f32(x1c.data_ptr(), x2c.data_ptr(), grad_out.data_ptr(), gbs, _ptr(act_out),
+                                     float(leaky_slope), _ptr(scratch), _ptr(g1), _ptr(g2), B, C, H, W, d,
+                                     _lib.stream_handle(x1.device))
+    _lib.check(rc, "usf_corr_bwd_ex_f32")
+    return g1, g2

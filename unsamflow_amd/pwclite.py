@@ -172,6 +172,10 @@ class PWCLite(nn.Module):
 
         self.feature_pyramid_extractor = FeatureExtractor(self.num_chs, input_adj_map=cfg.input_adj_map)
         self.corr = corr_module if corr_module is not None else _default_corr()
+        # the fused corr + LeakyReLU + concat op (corr_cat.py) stands in for the
+        # library's own Correlation module only; an injected module keeps the
+        # reference composition
+        self.fused_corr_cat = corr_module is None
         self.dim_corr = (2 * self.search_range + 1) ** 2
         self.num_ch_in = 32 + (2 if cfg.add_mask_corr else 1) * self.dim_corr + 2
         self.flow_estimators = (FlowEstimatorReduce if cfg.reduce_dense else FlowEstimatorDense)(self.num_ch_in)
@@ -213,14 +217,20 @@ class PWCLite(nn.Module):
                 x2_warp = self.warp(x2, flow)
             else:
                 x2_warp = x2
-            cost = self.leakyRELU(self.corr(x1, x2_warp))
-            feats = [cost]
+            pairs = [(x1, x2_warp)]
             if self.cfg.add_mask_corr:
                 m1 = self._mask_feature(x1, full_seg1, level)
                 m2 = self._mask_feature(x2, full_seg2, level)
-                feats.append(self.leakyRELU(self.corr(m1, self.warp(m2, flow))))
-            feats += [self.conv_1x1[level](x1), flow]
-            x_intm, flow_res = self.flow_estimators(torch.cat(feats, dim=1))
+                pairs.append((m1, self.warp(m2, flow)))
+            extras = [self.conv_1x1[level](x1), flow]
+            if self.fused_corr_cat and x1.is_cuda:
+                # LeakyReLU + concat fused into the correlation kernels (corr_cat.py)
+                from .corr_cat import corr_leaky_cat
+
+                est_in = corr_leaky_cat(pairs, extras, self.search_range, 0.1)
+            else:
+                est_in = torch.cat([self.leakyRELU(self.corr(a, b)) for a, b in pairs] + extras, dim=1)
+            x_intm, flow_res = self.flow_estimators(est_in)
             flow = flow + flow_res
             flow_fine, up_feat = self.context_networks(torch.cat([x_intm, flow], dim=1))
             flow = flow + flow_fine
