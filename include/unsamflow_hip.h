@@ -26,6 +26,9 @@
  *                        caller losses/flow_loss.py:101-103 (occ_from_back)
  *   usf_photo_loss_*  <- the per-scale warp + loss_photomatric composition of
  *                        losses/flow_loss.py:127-148
+ *   usf_flow_upsample_* <- F.interpolate(flow * k, scale_factor=k, bilinear,
+ *                        align_corners=True) of the decoder (pwclite.py:299-301;
+ *                        SURVEY §8f row 4)
  *
  * Contract (all entry points):
  *   - Pointers are DEVICE pointers to fp32 NCHW tensors. x/x1/x2/gout/out/gx*
@@ -164,6 +167,18 @@ int usf_photo_loss_bwd_f32(const float* src, const float* tgt, const float* mask
                            const float* flow, long long flow_bstride, const float* coef,
                            const float* grad_loss, float* grad_flow, int B, int C, int H,
                            int W, int pad_mode, void* stream);
+
+/* Decoder flow upsampling (pwclite.py:299-301 and the x4 output flows):
+ *   out = F.interpolate(flow * factor, scale_factor=factor, mode="bilinear",
+ *                       align_corners=True)
+ * flow: [B,C,H,W] dense; out: [B,C,H*factor,W*factor] dense, overwritten. */
+int usf_flow_upsample_f32(const float* flow, float* out, int B, int C, int H, int W,
+                          int factor, void* stream);
+
+/* Its backward: grad_flow [B,C,H,W] (overwritten, deterministic gather form)
+ * from grad_out [B,C,H*factor,W*factor]. */
+int usf_flow_upsample_bwd_f32(const float* grad_out, float* grad_flow, int B, int C, int H,
+                              int W, int factor, void* stream);
 
 /* Tuning hook (benchmarking only; not needed for correct use).
  * Forces kernel variant `index` of `op` for d=4 launches in this process:

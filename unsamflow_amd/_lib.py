@@ -71,6 +71,8 @@ _SIGNATURES = {
         [_c_float_p] * 4 + [ctypes.c_longlong] + [_c_float_p] * 3 + [ctypes.c_int] * 5 + [ctypes.c_void_p],
         ctypes.c_int,
     ),
+    "usf_flow_upsample_f32": ([_c_float_p] * 2 + [ctypes.c_int] * 5 + [ctypes.c_void_p], ctypes.c_int),
+    "usf_flow_upsample_bwd_f32": ([_c_float_p] * 2 + [ctypes.c_int] * 5 + [ctypes.c_void_p], ctypes.c_int),
     "usf_set_variant": ([ctypes.c_int, ctypes.c_int], ctypes.c_int),
 }
 EXPORTED_SYMBOLS = tuple(_SIGNATURES)

@@ -329,6 +329,42 @@ int usf_photo_loss_bwd_f32(const float* src, const float* tgt, const float* mask
                 (hipStream_t)stream);
 }
 
+int usf_flow_upsample_f32(const float* flow, float* out, int B, int C, int H, int W, int factor,
+                          void* stream) {
+  clear_error();
+  if (!check_dims("usf_flow_upsample_f32", B, C, H, W)) return USF_EINVAL;
+  if (factor < 1 || factor > 16 || (long long)C * H * W * factor * factor > 0x1FFFFFFBLL) {
+    set_error("usf_flow_upsample_f32: bad factor %d", factor);
+    return USF_EINVAL;
+  }
+  if (!flow || !out) {
+    set_error("usf_flow_upsample_f32: null pointer");
+    return USF_EINVAL;
+  }
+  if (const int pe = pre_check("usf_flow_upsample_f32", (hipStream_t)stream)) return pe;
+  return finish("usf_flow_upsample_f32",
+                upsample_fwd_launch(flow, out, B, C, H, W, factor, (hipStream_t)stream),
+                (hipStream_t)stream);
+}
+
+int usf_flow_upsample_bwd_f32(const float* grad_out, float* grad_flow, int B, int C, int H, int W,
+                              int factor, void* stream) {
+  clear_error();
+  if (!check_dims("usf_flow_upsample_bwd_f32", B, C, H, W)) return USF_EINVAL;
+  if (factor < 1 || factor > 16 || (long long)C * H * W * factor * factor > 0x1FFFFFFBLL) {
+    set_error("usf_flow_upsample_bwd_f32: bad factor %d", factor);
+    return USF_EINVAL;
+  }
+  if (!grad_out || !grad_flow) {
+    set_error("usf_flow_upsample_bwd_f32: null pointer");
+    return USF_EINVAL;
+  }
+  if (const int pe = pre_check("usf_flow_upsample_bwd_f32", (hipStream_t)stream)) return pe;
+  return finish("usf_flow_upsample_bwd_f32",
+                upsample_bwd_launch(grad_out, grad_flow, B, C, H, W, factor, (hipStream_t)stream),
+                (hipStream_t)stream);
+}
+
 int usf_set_variant(int op, int index) {
   clear_error();
   if (op < 0 || op > 2 || index < -1 || index >= variant_count(op)) {

@@ -1,0 +1,118 @@
+// Decoder flow upsampling for gfx950:
+//   F.interpolate(flow * k, scale_factor=k, mode="bilinear", align_corners=True)
+// (models/pwclite.py:299-301 between pyramid levels with k = 2, and the x4
+// output flows). Semantics of ATen's upsample_bilinear2d with
+// align_corners=True (third-party, torch 2.10): with the scale factor given,
+// the source scale is still (in - 1) / (out - 1) in fp32; src = scale * dst;
+// i0 = floor(src), i1 = i0 + (i0 < in - 1), l1 = src - i0, l0 = 1 - l1;
+// out = l0_y (l0_x v00 + l1_x v01) + l1_y (l0_x v10 + l1_x v11) with v = k * flow.
+// Forward: one lane per output element (coalesced writes, gathers from a
+// 4x smaller input). Backward: deterministic gather form -- each input element
+// sums the weights of the few output rows / columns whose taps reach it
+// (ATen scatters with atomics), times k.
+#include "usf_common.h"
+
+namespace usf {
+namespace {
+
+struct Lin {
+  int i0, i1;
+  float l0, l1;
+};
+
+__device__ __forceinline__ Lin lin_tap(int dst, float scale, int in) {
+#pragma clang fp contract(off)
+  const float src = scale * (float)dst;
+  Lin t;
+  t.i0 = (int)src;  // src >= 0: truncation == floor
+  t.i1 = t.i0 + (t.i0 < in - 1 ? 1 : 0);
+  t.l1 = src - (float)t.i0;
+  t.l0 = 1.f - t.l1;
+  return t;
+}
+
+__global__ __launch_bounds__(256) void upsample_fwd_kernel(const float* __restrict__ x,
+                                                           float* __restrict__ out, long long planes,
+                                                           int H, int W, int Ho, int Wo, float sy,
+                                                           float sx, float k) {
+#pragma clang fp contract(off)
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  const long long n = planes * Ho * Wo;
+  if (i >= n) return;
+  const int ox = (int)(i % Wo);
+  const int oy = (int)((i / Wo) % Ho);
+  const long long pl = i / ((long long)Ho * Wo);
+  const float* xp = x + pl * H * W;
+  const Lin ty = lin_tap(oy, sy, H), tx = lin_tap(ox, sx, W);
+  const float v00 = xp[ty.i0 * W + tx.i0] * k, v01 = xp[ty.i0 * W + tx.i1] * k;
+  const float v10 = xp[ty.i1 * W + tx.i0] * k, v11 = xp[ty.i1 * W + tx.i1] * k;
+  out[i] = ty.l0 * (tx.l0 * v00 + tx.l1 * v01) + ty.l1 * (tx.l0 * v10 + tx.l1 * v11);
+}
+
+// total weight output index `o` (tap t) gives input index `in_i` along one axis
+__device__ __forceinline__ float axis_weight(const Lin& t, int in_i) {
+  float w = 0.f;
+  if (t.i0 == in_i) w += t.l0;
+  if (t.i1 == in_i) w += t.l1;
+  return w;
+}
+
+__global__ __launch_bounds__(256) void upsample_bwd_kernel(const float* __restrict__ gout,
+                                                           float* __restrict__ gx, long long planes,
+                                                           int H, int W, int Ho, int Wo, float sy,
+                                                           float sx, float k) {
+#pragma clang fp contract(off)
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  const long long n = planes * H * W;
+  if (i >= n) return;
+  const int ix = (int)(i % W);
+  const int iy = (int)((i / W) % H);
+  const long long pl = i / ((long long)H * W);
+  const float* gp = gout + pl * Ho * Wo;
+  // output rows whose taps can touch input row iy: src in (iy - 1, iy + 1]
+  // (a generous window, filtered exactly by axis_weight)
+  const int oy0 = sy > 0.f ? max(0, (int)floorf((iy - 1) / sy) - 1) : 0;
+  const int oy1 = sy > 0.f ? min(Ho - 1, (int)ceilf((iy + 1) / sy) + 1) : Ho - 1;
+  const int ox0 = sx > 0.f ? max(0, (int)floorf((ix - 1) / sx) - 1) : 0;
+  const int ox1 = sx > 0.f ? min(Wo - 1, (int)ceilf((ix + 1) / sx) + 1) : Wo - 1;
+  float acc = 0.f;
+  for (int oy = oy0; oy <= oy1; ++oy) {
+    const float wy = axis_weight(lin_tap(oy, sy, H), iy);
+    if (wy == 0.f) continue;
+    float row = 0.f;
+    for (int ox = ox0; ox <= ox1; ++ox) {
+      const float wx = axis_weight(lin_tap(ox, sx, W), ix);
+      if (wx != 0.f) row += wx * gp[oy * Wo + ox];
+    }
+    acc += wy * row;
+  }
+  gx[i] = acc * k;
+}
+
+inline float ac_scale(int in, int out) {
+  return out > 1 ? (float)(in - 1) / (float)(out - 1) : 0.f;
+}
+
+}  // namespace
+
+hipError_t upsample_fwd_launch(const float* x, float* out, int B, int C, int H, int W, int k,
+                               hipStream_t s) {
+  const int Ho = H * k, Wo = W * k;
+  const long long planes = (long long)B * C;
+  const long long n = planes * Ho * Wo;
+  hipLaunchKernelGGL(upsample_fwd_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, x, out,
+                     planes, H, W, Ho, Wo, ac_scale(H, Ho), ac_scale(W, Wo), (float)k);
+  return hipGetLastError();
+}
+
+hipError_t upsample_bwd_launch(const float* gout, float* gx, int B, int C, int H, int W, int k,
+                               hipStream_t s) {
+  const int Ho = H * k, Wo = W * k;
+  const long long planes = (long long)B * C;
+  const long long n = planes * H * W;
+  hipLaunchKernelGGL(upsample_bwd_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, gout,
+                     gx, planes, H, W, Ho, Wo, ac_scale(H, Ho), ac_scale(W, Wo), (float)k);
+  return hipGetLastError();
+}
+
+}  // namespace usf

@@ -81,4 +81,9 @@ hipError_t photo_bwd_launch(const float* src, const float* tgt, const float* mas
                             long long flow_bstride, const float* coef, const float* gloss,
                             float* gflow, int B, int C, int H, int W, int pad_mode, hipStream_t s);
 
+hipError_t upsample_fwd_launch(const float* x, float* out, int B, int C, int H, int W, int k,
+                               hipStream_t s);
+hipError_t upsample_bwd_launch(const float* gout, float* gx, int B, int C, int H, int W, int k,
+                               hipStream_t s);
+
 }  // namespace usf

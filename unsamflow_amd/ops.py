@@ -348,3 +348,37 @@ def corr_backward_ex(x1: torch.Tensor, x2: torch.Tensor, grad_out: torch.Tensor,
                                      _lib.stream_handle(x1.device))
     _lib.check(rc, "usf_corr_bwd_ex_f32")
     return g1, g2
+
+
+def flow_upsample(flow: torch.Tensor, factor: int) -> torch.Tensor:
+    """F.interpolate(flow * factor, scale_factor=factor, mode="bilinear", align_corners=True)."""
+    _require_device_f32("flow", flow)
+    B, C, H, W = _nchw("flow", flow)
+    k = int(factor)
+    fc = flow.contiguous()
+    out = torch.empty((B, C, H * k, W * k), device=flow.device, dtype=torch.float32)
+    lib = _lib.load()
+    with torch.cuda.device(flow.device), _kt.timed("upsample", (B, C, H, W, k), flow.device,
+                                                     4 * B * C * H * W * (1 + k * k)):
+        rc = lib.usf_flow_upsample_f32(fc.data_ptr(), out.data_ptr(), B, C, H, W, k,
+                                       _lib.stream_handle(flow.device))
+    _lib.check(rc, "usf_flow_upsample_f32")
+    return out
+
+
+def flow_upsample_backward(grad_out: torch.Tensor, factor: int) -> torch.Tensor:
+    _require_device_f32("grad_out", grad_out)
+    B, C, Ho, Wo = _nchw("grad_out", grad_out)
+    k = int(factor)
+    if Ho % k or Wo % k:
+        raise ValueError(f"grad_out spatial size {(Ho, Wo)} is not a multiple of {k}")
+    H, W = Ho // k, Wo // k
+    gc = grad_out.contiguous()
+    gx = torch.empty((B, C, H, W), device=grad_out.device, dtype=torch.float32)
+    lib = _lib.load()
+    with torch.cuda.device(grad_out.device), _kt.timed("upsample_bwd", (B, C, H, W, k), grad_out.device,
+                                                         4 * B * C * H * W * (1 + k * k)):
+        rc = lib.usf_flow_upsample_bwd_f32(gc.data_ptr(), gx.data_ptr(), B, C, H, W, k,
+                                           _lib.stream_handle(grad_out.device))
+    _lib.check(rc, "usf_flow_upsample_bwd_f32")
+    return gx

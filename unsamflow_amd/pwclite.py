@@ -207,13 +207,22 @@ class PWCLite(nn.Module):
             return self.mask_aggregation(torch.cat((proj, spread), dim=1))
         raise NotImplementedError(self.cfg.aggregation_type)
 
+    def _upsample(self, flow, k):
+        """F.interpolate(flow * k, scale_factor=k, bilinear, align_corners=True) (:299-301);
+        the HIP op (upsample.py) next to the library's own corr/warp."""
+        if self.fused_corr_cat and flow.is_cuda:
+            from .upsample import upsample_flow
+
+            return upsample_flow(flow, k)
+        return F.interpolate(flow * k, scale_factor=k, mode="bilinear", align_corners=True)
+
     def decoder(self, x1_pyramid, x2_pyramid, full_seg1=None, full_seg2=None):
         flows = []
         B, _, h0, w0 = x1_pyramid[0].size()
         flow = torch.zeros(B, 2, h0, w0, dtype=x1_pyramid[0].dtype, device=x1_pyramid[0].device).float()
         for level, (x1, x2) in enumerate(zip(x1_pyramid, x2_pyramid)):
             if level > 0:
-                flow = F.interpolate(flow * 2, scale_factor=2, mode="bilinear", align_corners=True)
+                flow = self._upsample(flow, 2)
                 x2_warp = self.warp(x2, flow)
             else:
                 x2_warp = x2
@@ -237,7 +246,7 @@ class PWCLite(nn.Module):
             if self.output_flow_upsampler is not None:
                 flows.append(self.output_flow_upsampler(flow, up_feat))
             else:
-                flows.append(F.interpolate(flow * 4, scale_factor=4, mode="bilinear", align_corners=True))
+                flows.append(self._upsample(flow, 4))
             if level == self.output_level:
                 break
         return flows[::-1]
