@@ -154,6 +154,13 @@ def site_launcher(op: str, key, device, seed: int = 0):
         need1, need2 = key[4], key[5]
         go = torch.randn(B, 81, H, W, device=device, generator=g)
         return lambda: ops.corr_backward(x1, x2, go, 4, need1, need2)
+    if op in ("upsample", "upsample_bwd"):
+        B, C, H, W, k = key[:5]
+        if op == "upsample":
+            f = torch.randn(B, C, H, W, device=device, generator=g)
+            return lambda: ops.flow_upsample(f, k)
+        go = torch.randn(B, C, H * k, W * k, device=device, generator=g)
+        return lambda: ops.flow_upsample_backward(go, k)
     if op in ("occ_bwd", "splat", "photo_fwd", "photo_bwd"):
         B, C, H, W = key[:4]
         yy = torch.linspace(0, 6.2832, H, device=device).view(1, 1, H, 1)
