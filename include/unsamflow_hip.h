@@ -57,7 +57,7 @@
 extern "C" {
 #endif
 
-#define USF_ABI_VERSION 1
+#define USF_ABI_VERSION 2
 #define USF_EINVAL (-1)
 
 /* padding modes for the warp (flow_warp `pad` argument) */
@@ -152,21 +152,37 @@ int usf_occ_backward_f32(const float* flow21, long long flow_bstride, float* occ
  * src, tgt: [B,C,H,W] dense, 1 <= C <= 3 (images); mask: [B,1,H,W] dense; flow:
  * [B,2,H,W] with batch stride flow_bstride. partials: caller scratch of
  * usf_photo_loss_partials(B,H,W) floats. out: 3 floats = {L, c_l1, c_ssim}
- * (c_* are what the backward needs). Deterministic (fixed-order sums). */
+ * (c_* are what the backward needs). grad_basis: NULL (no gradient wanted), or
+ * [B,4,H,W] dense, overwritten with the per-pixel flow-gradient basis
+ * {A_x, A_y, S_x, S_y}: dL/dflow = c_l1 * A + c_ssim * S (the L1 and the SSIM
+ * parts; L is linear in both), computed in the same pass. Deterministic
+ * (fixed-order sums). usf_photo_loss_partials(B,H,W) is per direction. */
 int usf_photo_loss_partials(int B, int H, int W);
 int usf_photo_loss_fwd_f32(const float* src, const float* tgt, const float* mask,
                            const float* flow, long long flow_bstride, float* partials,
-                           float* out, int B, int C, int H, int W, int pad_mode,
-                           float w_l1, float w_ssim, void* stream);
+                           float* out, float* grad_basis, int B, int C, int H, int W,
+                           int pad_mode, float w_l1, float w_ssim, void* stream);
 
-/* Backward of usf_photo_loss_fwd_f32 w.r.t. the flow only (the mask and the
- * images carry no gradient): grad_flow = dL/dflow * (*grad_loss).
- * coef: the `out` of the forward (device pointer); grad_loss: device scalar;
- * grad_flow: [B,2,H,W] dense, overwritten, deterministic. */
-int usf_photo_loss_bwd_f32(const float* src, const float* tgt, const float* mask,
-                           const float* flow, long long flow_bstride, const float* coef,
-                           const float* grad_loss, float* grad_flow, int B, int C, int H,
-                           int W, int pad_mode, void* stream);
+/* Both directions of a with_bk scale in one launch (flow_loss.py:130-131,
+ * 176-178 of the unFlowLoss): direction 0 warps im2 by flow[:, 0:2] onto im1
+ * under mask1, direction 1 warps im1 by flow[:, 2:4] onto im2 under mask2.
+ * flow: [B,4,H,W] with batch stride flow_bstride (dense [4,H,W] per sample);
+ * partials: 2 * usf_photo_loss_partials(B,H,W) floats; out: 6 floats
+ * {L, c_l1, c_ssim} per direction; grad_basis: NULL or [B,2,4,H,W] dense. */
+int usf_photo_loss_pair_fwd_f32(const float* im1, const float* im2, const float* mask1,
+                                const float* mask2, const float* flow, long long flow_bstride,
+                                float* partials, float* out, float* grad_basis, int B, int C,
+                                int H, int W, int pad_mode, float w_l1, float w_ssim,
+                                void* stream);
+
+/* Backward of usf_photo_loss_fwd_f32 (ndir = 1) or _pair_fwd_f32 (ndir = 2)
+ * w.r.t. the flow only (the mask and the images carry no gradient):
+ * grad_flow[:, 2d:2d+2] = (c_l1 * A + c_ssim * S) * grad_loss[d] per direction d.
+ * grad_basis: the forward's [B,ndir,4,H,W] basis; coef: the forward's `out`
+ * (3 * ndir floats, device); grad_loss: ndir device floats; grad_flow:
+ * [B,2*ndir,H,W] dense, overwritten, deterministic. */
+int usf_photo_loss_bwd_f32(const float* grad_basis, const float* coef, const float* grad_loss,
+                           float* grad_flow, int B, int H, int W, int ndir, void* stream);
 
 /* Decoder flow upsampling (pwclite.py:299-301 and the x4 output flows):
  *   out = F.interpolate(flow * factor, scale_factor=factor, mode="bilinear",

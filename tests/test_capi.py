@@ -33,7 +33,8 @@ def test_header_declares_the_abi():
         ["usf_abi_version", "usf_last_error_string", "usf_corr_fwd_f32", "usf_corr_bwd_f32",
          "usf_corr_fwd_ex_f32", "usf_corr_bwd_ex_f32",
          "usf_warp_fwd_f32", "usf_warp_bwd_f32", "usf_splat_map_f32", "usf_occ_backward_f32",
-         "usf_photo_loss_partials", "usf_photo_loss_fwd_f32", "usf_photo_loss_bwd_f32",
+         "usf_photo_loss_partials", "usf_photo_loss_fwd_f32", "usf_photo_loss_pair_fwd_f32",
+         "usf_photo_loss_bwd_f32",
          "usf_flow_upsample_f32", "usf_flow_upsample_bwd_f32",
          "usf_set_variant"]
     )
@@ -54,7 +55,7 @@ def test_library_exports_every_declared_symbol(lib):
 def test_abi_version(lib):
     from unsamflow_amd import _lib
 
-    assert lib.usf_abi_version() == _lib.ABI_VERSION == 1
+    assert lib.usf_abi_version() == _lib.ABI_VERSION == 2
 
 
 def test_no_torch_types_in_abi():
@@ -88,10 +89,14 @@ def test_no_torch_types_in_abi():
         (lambda L: L.usf_splat_map_f32(None, 2 * 16, 1, 1, 4, 4, 0, None), "null pointer"),
         (lambda L: L.usf_occ_backward_f32(1, 3, 1, 2, 4, 4, 0.2, None), "batch stride"),
         (lambda L: L.usf_occ_backward_f32(1, 32, None, 1, 4, 4, 0.2, None), "null pointer"),
-        (lambda L: L.usf_photo_loss_fwd_f32(1, 1, 1, 1, 32, 1, 1, 1, 4, 4, 4, 1, 0.15, 0.85, None), "> 3"),
-        (lambda L: L.usf_photo_loss_fwd_f32(1, 1, 1, 1, 32, 1, 1, 1, 3, 4, 4, 9, 0.15, 0.85, None), "pad_mode 9"),
-        (lambda L: L.usf_photo_loss_fwd_f32(1, None, 1, 1, 32, 1, 1, 1, 3, 4, 4, 1, 0.15, 0.85, None), "null input"),
-        (lambda L: L.usf_photo_loss_bwd_f32(1, 1, 1, 1, 32, None, 1, 1, 1, 3, 4, 4, 1, None), "null pointer"),
+        (lambda L: L.usf_photo_loss_fwd_f32(1, 1, 1, 1, 32, 1, 1, None, 1, 4, 4, 4, 1, 0.15, 0.85, None), "> 3"),
+        (lambda L: L.usf_photo_loss_fwd_f32(1, 1, 1, 1, 32, 1, 1, 1, 1, 3, 4, 4, 9, 0.15, 0.85, None), "pad_mode 9"),
+        (lambda L: L.usf_photo_loss_fwd_f32(1, None, 1, 1, 32, 1, 1, None, 1, 3, 4, 4, 1, 0.15, 0.85, None), "null input"),
+        (lambda L: L.usf_photo_loss_bwd_f32(1, None, 1, 1, 1, 4, 4, 1, None), "null pointer"),
+        (lambda L: L.usf_photo_loss_bwd_f32(1, 1, 1, 1, 0, 4, 4, 1, None), "non-positive"),
+        (lambda L: L.usf_photo_loss_bwd_f32(1, 1, 1, 1, 1, 4, 4, 3, None), "ndir=3"),
+        (lambda L: L.usf_photo_loss_pair_fwd_f32(1, 1, 1, 1, 1, 32, 1, 1, None, 2, 3, 4, 4, 1, 0.15, 0.85, None), "< 4*H*W"),
+        (lambda L: L.usf_photo_loss_pair_fwd_f32(1, 1, 1, None, 1, 64, 1, 1, None, 2, 3, 4, 4, 1, 0.15, 0.85, None), "null input"),
     ],
 )
 def test_invalid_arguments_rejected_without_launch(lib, call, needle):

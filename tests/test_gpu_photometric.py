@@ -87,3 +87,62 @@ def test_photometric_loss_in_unflowloss_matches_torch_path(hip_device):
         assert (a is None) == (b is None)
         if a is not None:
             np.testing.assert_allclose(a, b, rtol=1e-3, atol=2e-4 * max(float(np.abs(b).max()), 1e-12))
+
+
+PAIR_CASES = [
+    (2, 3, 24, 40, 2.0, "border"),
+    (1, 3, 3, 5, 1.0, "border"),
+    (2, 1, 33, 47, 3.0, "zeros"),
+    (8, 3, 64, 208, 4.0, "border"),
+]
+
+
+@pytest.mark.parametrize("B,C,H,W,scale,pad", PAIR_CASES)
+def test_photometric_pair_matches_reference_and_single_directions(hip_device, B, C, H, W, scale, pad):
+    """Both with_bk directions in one launch == the two single-direction calls
+    (bit-identical: same kernel body per direction) and == the reference
+    composition of each direction (flow_loss.py:130-131, 176-178)."""
+    from unsamflow_amd.photometric import photometric_loss, photometric_loss_pair
+
+    seed = 300 + H + W
+    im1 = torch.from_numpy(hashrng.uniform((B, C, H, W), seed))
+    im2 = torch.from_numpy(hashrng.uniform((B, C, H, W), seed + 1))
+    flow = torch.from_numpy(hashrng.symmetric((B, 4, H, W), seed + 2, scale))
+    m1 = (torch.from_numpy(hashrng.uniform((B, 1, H, W), seed + 3)) > 0.2).float()
+    m2 = (torch.from_numpy(hashrng.uniform((B, 1, H, W), seed + 4)) > 0.3).float()
+    d = hip_device
+
+    fp = flow.to(d).requires_grad_(True)
+    lp = photometric_loss_pair(fp, im1.to(d), im2.to(d), m1.to(d), m2.to(d), pad, 0.15, 0.85)
+    (lp[0] * 0.7 + lp[1] * 1.3).backward()
+
+    fs = flow.to(d).requires_grad_(True)
+    l0 = photometric_loss(fs[:, :2], im2.to(d), im1.to(d), m1.to(d), pad, 0.15, 0.85)
+    l1 = photometric_loss(fs[:, 2:], im1.to(d), im2.to(d), m2.to(d), pad, 0.15, 0.85)
+    (l0 * 0.7 + l1 * 1.3).backward()
+    assert torch.equal(lp.detach().cpu(), torch.stack([l0, l1]).detach().cpu())
+    assert torch.equal(fp.grad.cpu(), fs.grad.cpu())
+
+    fr = flow.clone().requires_grad_(True)
+    r0 = _ref_loss(fr[:, :2], im2, im1, m1, pad, 0.15, 0.85)
+    r1 = _ref_loss(fr[:, 2:], im1, im2, m2, pad, 0.15, 0.85)
+    (r0 * 0.7 + r1 * 1.3).backward()
+    np.testing.assert_allclose(lp.detach().cpu().numpy(), [float(r0), float(r1)], rtol=2e-5, atol=0)
+    gref = fr.grad.numpy()
+    np.testing.assert_allclose(fp.grad.cpu().numpy(), gref, rtol=1e-3, atol=2e-4 * float(np.abs(gref).max()))
+
+
+def test_photometric_forward_only_matches_grad_forward(hip_device):
+    """The no-grad instantiation (no basis) computes the same loss value (up to
+    FMA contraction choices of the two instantiations)."""
+    from unsamflow_amd import ops
+
+    B, C, H, W = 2, 3, 40, 72
+    src = torch.from_numpy(hashrng.uniform((B, C, H, W), 7)).to(hip_device)
+    tgt = torch.from_numpy(hashrng.uniform((B, C, H, W), 8)).to(hip_device)
+    flow = torch.from_numpy(hashrng.symmetric((B, 2, H, W), 9, 3.0)).to(hip_device)
+    mask = (torch.from_numpy(hashrng.uniform((B, 1, H, W), 10)) > 0.2).float().to(hip_device)
+    a, basis = ops.photo_loss_forward(src, tgt, mask, flow, "border", need_grad=True)
+    b, none = ops.photo_loss_forward(src, tgt, mask, flow, "border", need_grad=False)
+    assert none is None and basis.shape == (B, 4, H, W)
+    np.testing.assert_allclose(a.cpu().numpy(), b.cpu().numpy(), rtol=1e-6, atol=0)

@@ -19,7 +19,9 @@ SITES += [("warp_bwd", (8, C, H, W, "border", True, True)) for C, H, W in KITTI[
 SITES += [("warp_fwd", (8, 3, 256, 832, "border")), ("warp_bwd", (8, 3, 256, 832, "border", False, True))]
 SITES += [("occ_bwd", (8, 1, 256, 832))]
 SITES += [("photo_fwd", (8, 3, 256 >> i, 832 >> i, "border")) for i in range(4)]
-SITES += [("photo_bwd", (8, 3, 256 >> i, 832 >> i, "border")) for i in range(4)]
+SITES += [("photo_fwd_grad", (8, 3, 256 >> i, 832 >> i, "border")) for i in range(4)]
+SITES += [("photo_pair_grad", (8, 3, 256 >> i, 832 >> i, "border")) for i in range(4)]
+SITES += [("photo_bwd", (8, 2, 256 >> i, 832 >> i)) for i in range(4)]
 
 
 def main():
@@ -31,7 +33,9 @@ def main():
     b = torch.empty_like(a)
     for _ in range(n):
         b.copy_(a)
-    for op, key in SITES:
+    only = os.environ.get("KPROF_OPS")  # e.g. "photo_fwd_grad,photo_bwd": a subset of the sites
+    sites = [s for s in SITES if not only or s[0] in only.split(",")]
+    for op, key in sites:
         fn = site_launcher(op, key, dev)
         for _ in range(n):
             fn()

@@ -4,7 +4,7 @@ Input: the FETCH_SIZE and WRITE_SIZE passes of tools/gpu_pmc.sh over
 tools/kprof.py (each its own rocprofv3 --pmc run with --kernel-trace only).
 kprof.py launches, in order: a 256 MiB device copy (n times, calibration),
 then every site of kprof.SITES n times; each site launch contains exactly one
-usf:: kernel (two for occ_bwd and photo_fwd), so usf dispatches map to sites
+usf:: kernel (two for occ_bwd and photo_fwd[_grad]), so usf dispatches map to sites
 by order.
 
 Correction (MI355X_MICROARCH.md, HBM/rocprofv3): FETCH_SIZE under-reports
@@ -57,10 +57,9 @@ def main():
     uf = [v for name, v in fetch if "usf::" in name]
     uw = [v for name, v in write if "usf::" in name]
     # library kernels per launch of a site (summed): splat + threshold, partials + final
-    per_launch = {"occ_bwd": 2, "photo_fwd": 2}
-    # kernels a site's launcher runs once before its timed launches (photo_bwd:
-    # one forward = 2 kernels for the coefficients)
-    prefix = {"photo_bwd": 2}
+    per_launch = {"occ_bwd": 2, "photo_fwd": 2, "photo_fwd_grad": 2, "photo_pair_grad": 2}
+    # kernels a site's launcher runs once before its timed launches
+    prefix = {}
     sites, pos = [], 0
     for op, key in SITES:
         k = per_launch.get(op, 1)
@@ -68,7 +67,10 @@ def main():
         fk = statistics.median(sum(uf[pos + j * k + i] for i in range(k)) for j in range(n))
         wk = statistics.median(sum(uw[pos + j * k + i] for i in range(k)) for j in range(n))
         pos += k * n
-        B, C, H, W = key[:4]
+        if op == "photo_bwd":
+            B, ndir, H, W = key
+        else:
+            B, C, H, W = key[:4]
         if op.startswith("corr"):
             alg = corr_bytes(*key[:4], backward=op == "corr_bwd")
         elif op == "warp_fwd":
@@ -79,8 +81,12 @@ def main():
             alg = 4 * B * H * W * 3  # flow in, mask out (ops.occ_backward)
         elif op == "photo_fwd":
             alg = 4 * B * H * W * (2 * C + 3)
+        elif op == "photo_fwd_grad":
+            alg = 4 * B * H * W * (2 * C + 7)  # + the [B,4,H,W] gradient basis written
+        elif op == "photo_pair_grad":
+            alg = 2 * 4 * B * H * W * (2 * C + 7)  # both directions
         else:
-            alg = 4 * B * H * W * (2 * C + 5)
+            alg = 4 * B * H * W * 6 * ndir  # photo_bwd: basis in, grad_flow out
         traffic = fk * 1024 * f_read + wk * 1024 * f_write
         sites.append({"op": op, "shape": list(key), "fetch_kib": round(fk, 1), "write_kib": round(wk, 1),
                       "traffic_bytes": int(traffic), "algorithmic_bytes": int(alg),

@@ -1,0 +1,92 @@
+"""Device time of selected hot-path call sites at PWCLite's B=8 KITTI shapes
+(graph-replayed launches, HIP events; unsamflow_amd.kernel_timer), with the
+algorithmic GB/s and HBM fraction of each.
+
+Usage (GPU box): python tools/sitebench.py [--ops photo_fwd_grad,photo_bwd,...]
+                 [--out gpurun_out/sitebench.json]
+"""
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+from unsamflow_amd import _lib  # noqa: E402
+from unsamflow_amd.kernel_timer import device_time_us, site_launcher  # noqa: E402
+
+KITTI = [(192, 4, 13), (128, 8, 26), (96, 16, 52), (64, 32, 104), (32, 64, 208)]
+SCALES = [(256 >> i, 832 >> i) for i in range(4)]
+
+
+def site_list(ops):
+    out = []
+    for op in ops:
+        if op == "corr_fwd":
+            out += [(op, (8, C, H, W)) for C, H, W in KITTI]
+        elif op == "corr_bwd":
+            out += [(op, (8, C, H, W, True, True)) for C, H, W in KITTI]
+        elif op == "warp_fwd":
+            out += [(op, (8, C, H, W, "border")) for C, H, W in KITTI[1:]]
+        elif op == "warp_bwd":
+            out += [(op, (8, C, H, W, "border", True, True)) for C, H, W in KITTI[1:]]
+        elif op in ("photo_fwd", "photo_fwd_grad", "photo_pair", "photo_pair_grad"):
+            out += [(op, (8, 3, H, W, "border")) for H, W in SCALES]
+        elif op == "photo_bwd":
+            out += [(op, (8, 2, H, W)) for H, W in SCALES]
+        elif op == "occ_bwd":
+            out += [(op, (8, 1, 256, 832))]
+        else:
+            raise SystemExit(f"unknown op {op}")
+    return out
+
+
+def alg_bytes(op, key):
+    if op == "photo_bwd":
+        B, ndir, H, W = key
+        return 4 * B * H * W * 6 * ndir
+    B, C, H, W = key[:4]
+    if op == "corr_fwd":
+        return 4 * B * H * W * (2 * C + 81)
+    if op == "corr_bwd":
+        return 4 * B * H * W * (81 + 4 * C)
+    if op == "warp_fwd":
+        return 4 * B * H * W * (2 * C + 2)
+    if op == "warp_bwd":
+        return 4 * B * H * W * (3 * C + 4)
+    if op == "photo_fwd":
+        return 4 * B * H * W * (2 * C + 3)
+    if op == "photo_fwd_grad":
+        return 4 * B * H * W * (2 * C + 7)
+    if op == "photo_pair":
+        return 2 * 4 * B * H * W * (2 * C + 3)
+    if op == "photo_pair_grad":
+        return 2 * 4 * B * H * W * (2 * C + 7)
+    if op == "occ_bwd":
+        return 4 * B * H * W * 3
+    raise KeyError(op)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--ops", default="photo_pair,photo_pair_grad,photo_bwd")
+    ap.add_argument("--out", default="gpurun_out/sitebench.json")
+    a = ap.parse_args()
+    _lib.load()
+    dev = torch.device("cuda:0")
+    rows = []
+    for i, (op, key) in enumerate(site_list(a.ops.split(","))):
+        us = device_time_us(site_launcher(op, key, dev, seed=i))
+        nb = alg_bytes(op, key)
+        row = {"op": op, "shape": list(key), "device_us": round(us, 2), "bytes": nb,
+               "gbps": round(nb / us / 1e3, 1), "hbm_frac": round(nb / us / 1e3 / 8000.0, 4)}
+        rows.append(row)
+        print(json.dumps(row), flush=True)
+    os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
+    with open(a.out, "w") as f:
+        json.dump(rows, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

@@ -17,7 +17,7 @@ from pathlib import Path
 import torch  # noqa: F401  (load torch's HIP runtime before the plugin)
 
 _LIB_PATH = Path(os.environ.get("USF_LIB", Path(__file__).resolve().parent / "lib" / "libunsamflow_hip.so"))
-ABI_VERSION = 1
+ABI_VERSION = 2
 PAD_ZEROS = 0
 PAD_BORDER = 1
 
@@ -63,12 +63,17 @@ _SIGNATURES = {
     ),
     "usf_photo_loss_partials": ([ctypes.c_int] * 3, ctypes.c_int),
     "usf_photo_loss_fwd_f32": (
-        [_c_float_p] * 4 + [ctypes.c_longlong, _c_float_p, _c_float_p] + [ctypes.c_int] * 5
+        [_c_float_p] * 4 + [ctypes.c_longlong, _c_float_p, _c_float_p, _c_float_p] + [ctypes.c_int] * 5
+        + [ctypes.c_float, ctypes.c_float, ctypes.c_void_p],
+        ctypes.c_int,
+    ),
+    "usf_photo_loss_pair_fwd_f32": (
+        [_c_float_p] * 5 + [ctypes.c_longlong, _c_float_p, _c_float_p, _c_float_p] + [ctypes.c_int] * 5
         + [ctypes.c_float, ctypes.c_float, ctypes.c_void_p],
         ctypes.c_int,
     ),
     "usf_photo_loss_bwd_f32": (
-        [_c_float_p] * 4 + [ctypes.c_longlong] + [_c_float_p] * 3 + [ctypes.c_int] * 5 + [ctypes.c_void_p],
+        [_c_float_p] * 4 + [ctypes.c_int] * 4 + [ctypes.c_void_p],
         ctypes.c_int,
     ),
     "usf_flow_upsample_f32": ([_c_float_p] * 2 + [ctypes.c_int] * 5 + [ctypes.c_void_p], ctypes.c_int),

@@ -296,8 +296,9 @@ static bool check_photo(const char* fn, const float* src, const float* tgt, cons
 }
 
 int usf_photo_loss_fwd_f32(const float* src, const float* tgt, const float* mask, const float* flow,
-                           long long flow_bstride, float* partials, float* out, int B, int C, int H,
-                           int W, int pad_mode, float w_l1, float w_ssim, void* stream) {
+                           long long flow_bstride, float* partials, float* out, float* grad_basis,
+                           int B, int C, int H, int W, int pad_mode, float w_l1, float w_ssim,
+                           void* stream) {
   clear_error();
   if (!check_photo("usf_photo_loss_fwd_f32", src, tgt, mask, flow, flow_bstride, B, C, H, W, pad_mode))
     return USF_EINVAL;
@@ -307,25 +308,53 @@ int usf_photo_loss_fwd_f32(const float* src, const float* tgt, const float* mask
   }
   if (const int pe = pre_check("usf_photo_loss_fwd_f32", (hipStream_t)stream)) return pe;
   return finish("usf_photo_loss_fwd_f32",
-                photo_fwd_launch(src, tgt, mask, flow, flow_bstride, partials, out, B, C, H, W,
-                                 pad_mode, w_l1, w_ssim, (hipStream_t)stream),
+                photo_fwd_launch(src, tgt, mask, flow, flow_bstride, partials, out, grad_basis, B, C,
+                                 H, W, pad_mode, w_l1, w_ssim, (hipStream_t)stream),
                 (hipStream_t)stream);
 }
 
-int usf_photo_loss_bwd_f32(const float* src, const float* tgt, const float* mask, const float* flow,
-                           long long flow_bstride, const float* coef, const float* grad_loss,
-                           float* grad_flow, int B, int C, int H, int W, int pad_mode, void* stream) {
+int usf_photo_loss_pair_fwd_f32(const float* im1, const float* im2, const float* mask1,
+                                const float* mask2, const float* flow, long long flow_bstride,
+                                float* partials, float* out, float* grad_basis, int B, int C, int H,
+                                int W, int pad_mode, float w_l1, float w_ssim, void* stream) {
   clear_error();
-  if (!check_photo("usf_photo_loss_bwd_f32", src, tgt, mask, flow, flow_bstride, B, C, H, W, pad_mode))
+  const char* fn = "usf_photo_loss_pair_fwd_f32";
+  if (!check_photo(fn, im1, im2, mask1, flow, flow_bstride, B, C, H, W, pad_mode)) return USF_EINVAL;
+  if (!mask2) {
+    set_error("%s: null input pointer", fn);
     return USF_EINVAL;
-  if (!coef || !grad_loss || !grad_flow) {
+  }
+  if (flow_bstride < 4LL * H * W && B > 1) {
+    set_error("%s: flow batch stride %lld < 4*H*W", fn, flow_bstride);
+    return USF_EINVAL;
+  }
+  if (!partials || !out) {
+    set_error("%s: null output pointer", fn);
+    return USF_EINVAL;
+  }
+  if (const int pe = pre_check(fn, (hipStream_t)stream)) return pe;
+  return finish(fn,
+                photo_pair_fwd_launch(im1, im2, mask1, mask2, flow, flow_bstride, partials, out,
+                                      grad_basis, B, C, H, W, pad_mode, w_l1, w_ssim,
+                                      (hipStream_t)stream),
+                (hipStream_t)stream);
+}
+
+int usf_photo_loss_bwd_f32(const float* grad_basis, const float* coef, const float* grad_loss,
+                           float* grad_flow, int B, int H, int W, int ndir, void* stream) {
+  clear_error();
+  if (!check_dims("usf_photo_loss_bwd_f32", B, 8, H, W)) return USF_EINVAL;
+  if (ndir != 1 && ndir != 2) {
+    set_error("usf_photo_loss_bwd_f32: ndir=%d (1 or 2)", ndir);
+    return USF_EINVAL;
+  }
+  if (!grad_basis || !coef || !grad_loss || !grad_flow) {
     set_error("usf_photo_loss_bwd_f32: null pointer");
     return USF_EINVAL;
   }
   if (const int pe = pre_check("usf_photo_loss_bwd_f32", (hipStream_t)stream)) return pe;
   return finish("usf_photo_loss_bwd_f32",
-                photo_bwd_launch(src, tgt, mask, flow, flow_bstride, coef, grad_loss, grad_flow, B, C,
-                                 H, W, pad_mode, (hipStream_t)stream),
+                photo_bwd_launch(grad_basis, coef, grad_loss, grad_flow, B, H, W, ndir, (hipStream_t)stream),
                 (hipStream_t)stream);
 }
 

@@ -1,6 +1,7 @@
 // Fused occlusion-aware photometric loss of unFlowLoss for gfx950 (CDNA4):
-// the per-scale, per-direction term of losses/flow_loss.py:127-148 with
-// loss_photomatric (:33-50) and SSIM (losses/loss_blocks.py:53-72):
+// the per-scale term of losses/flow_loss.py:127-148 with loss_photomatric
+// (:33-50) and SSIM (losses/loss_blocks.py:53-72), for one flow direction or
+// for both directions of a with_bk scale in one launch:
 //
 //   rec  = flow_warp(src, flow, pad)                      (warp_utils.py:97-106)
 //   x    = rec * m,  y = tgt * m                          (SSIM arguments, :40)
@@ -12,16 +13,36 @@
 //          d = (mu_x^2 + mu_y^2 + C1)(sig_x + sig_y + C2), C1 = 0.01^2, C2 = 0.03^2
 //
 // The mask m and tgt carry no gradient (the reference thresholds the mask);
-// only the flow does. Forward: one kernel per (16x16 tile, sample) warps the
-// source for the tile + 2-pixel halo straight into LDS, sums the L1, SSIM and
-// mask terms and writes per-block partials; a one-block kernel combines them
-// in a fixed order (fp64) into the loss and the two backward coefficients.
-// Backward: dS_q/dx_p = alpha_q + beta_q x_p + gamma_q y_p (closed form below),
-// so one kernel per tile stages x/y for the tile + 2-pixel halo, the window
-// coefficients for the tile + 1-pixel halo, sums the 9 windows around each
-// pixel, adds the L1 sign term and folds dL/drec through the bilinear
-// coordinate derivative into grad_flow -- the warp's grad_flow path of
-// warp.hip, without materialising rec, the SSIM maps or dL/drec in HBM.
+// only the flow does, and L is linear in its two normalised sums, so
+//   dL/dflow_p = c_l1 * A_p + c_ssim * S'_p
+// with the per-pixel vectors (dI/dflow = the bilinear tap's coordinate
+// derivative incl. norm_grid and the border clip, as in warp.hip)
+//   A_p  = m_p * sum_c sign(rec_pc - tgt_pc) * dI_pc/dflow
+//   S'_p = m_p * sum_c (sum_{q ∋ p} dS_q/dx_pc) * dI_pc/dflow
+// and the scalars c_l1 = w_l1 / (N_l1 (mean m + 1e-6)), c_ssim likewise, which
+// are known only after the global reduction. So ONE pass does all the work:
+// photo_fwd_kernel<GRAD> warps the source for a 32x16 tile + 2-pixel halo
+// straight into LDS (x, y), sums the L1, SSIM and mask terms into per-tile
+// partials and, when the flow needs a gradient, also evaluates the closed form
+// dS_q/dx_p = alpha_q + beta_q x_p + gamma_q y_p per window, box-sums it around
+// every pixel and writes the 4-float basis {A_p, S'_p} (16 B/pixel). A one-block
+// (per direction) kernel combines the partials in a fixed fp64 order into
+// {L, c_l1, c_ssim}; the backward is then a dense 24 B/pixel pass,
+// gflow = g (c_l1 A + c_ssim S'). Nothing is recomputed between forward and
+// backward and no warped image, SSIM map or dL/drec reaches HBM.
+// Deterministic: fixed-order sums, no atomics.
+//
+// Work split (256 threads): the owner thread stages its two vertically
+// adjacent pixels and keeps their tap derivatives in registers (no second
+// flow / image read); the 208-pixel halo ring is one more staging pass. All
+// global loads of the staging are issued before their first use
+// (unconditional loads at clamped in-bounds offsets), so a workgroup pays the
+// flow -> gather latency chain once. Windows are evaluated column-wise, three
+// stacked windows per thread from five horizontal row sums (one pass over the
+// 34 x 18 window grid); the pixel box sums reuse the overlap of the owner's two
+// pixels. Window statistics use FMAs and a hardware reciprocal (the loss is
+// checked against the reference at a stated tolerance); the warp coordinate
+// chain keeps the reference rounding (warp_tap.h).
 #include <cstdint>
 
 #include "usf_common.h"
@@ -30,366 +51,478 @@
 namespace usf {
 namespace {
 
-constexpr int kTile = 16;              // 16x16 output pixels per workgroup (256 threads)
-constexpr int kMaxC = 3;               // image channels per pixel (RGB; LDS is sized for 3)
-constexpr float kC1 = 0.01f * 0.01f;   // torch casts the python scalars to fp32
+constexpr int kTW = 32, kTH = 16;              // own tile: 32 x 16 pixels, 2 per thread
+constexpr int kRW = kTW + 4, kRH = kTH + 4;    // x / y region: 2-pixel halo
+constexpr int kWW = kTW + 2, kWH = kTH + 2;    // windows (top-left) the tile's pixels touch
+constexpr int kXS = kRW + 1;                   // LDS row strides
+constexpr int kAS = kWW + 1;
+constexpr int kHalo = kRW * kRH - kTW * kTH;   // 208 halo pixels
+constexpr int kWG = 3;                         // stacked windows per thread (window phase)
+constexpr int kWItems = kWW * (kWH / kWG);     // 204 column items
+constexpr int kNT = 256;
+constexpr int kMaxC = 3;                       // image channels per pixel (RGB; LDS is sized for 3)
+constexpr float kC1 = 0.01f * 0.01f;           // torch casts the python scalars to fp32
 constexpr float kC2 = 0.03f * 0.03f;
+static_assert(kHalo <= kNT && kWItems <= kNT && kWH % kWG == 0, "one pass per phase");
 
-// bilinear sample of the C channels of src at pixel (px, py) displaced by the
-// flow, with the reference's coordinate chain (warp_tap.h); also returns the tap
-__device__ __forceinline__ void sample_px(const float* __restrict__ srcb, const float* __restrict__ fb,
-                                          int px, int py, int H, int W, int C, bool border,
-                                          float (&out)[kMaxC], Tap& tp) {
-#pragma clang fp contract(off)
+// one flow direction: rec = warp(src, flow), compared with tgt under mask
+struct PhotoDir {
+  const float* src;
+  const float* tgt;
+  const float* mask;
+  const float* flow;  // [2,H,W] block per sample at flow + b * fbs
+  float* basis;       // 4 planes per sample at basis + b * bbs, or null (forward only)
+};
+struct PhotoArgs {
+  PhotoDir dir[2];
+  long long fbs, bbs;  // flow / basis batch strides (elements)
+  int B, C, H, W, tiles_x;
+};
+
+// region coordinates of halo element h (top 2 rows, bottom 2 rows, left 2 cols, right 2 cols)
+__device__ __forceinline__ void halo_coord(int h, int& ry, int& rx) {
+  if (h < 2 * kRW) {
+    ry = h / kRW; rx = h - ry * kRW;
+  } else if (h < 4 * kRW) {
+    h -= 2 * kRW; ry = kRH - 2 + h / kRW; rx = h % kRW;
+  } else if (h < 4 * kRW + 2 * kTH) {
+    h -= 4 * kRW; ry = 2 + (h >> 1); rx = h & 1;
+  } else {
+    h -= 4 * kRW + 2 * kTH; ry = 2 + (h >> 1); rx = kRW - 2 + (h & 1);
+  }
+}
+
+// One staged pixel: the reference coordinate chain (warp_tap.h), the 4 corner
+// gathers of every channel and the target, all loads unconditional at
+// clamped in-bounds offsets so they issue back to back.
+struct Px {
+  Tap tp;
+  float m;
+  float v[kMaxC][4];  // corners nw, ne, sw, se (0 where masked)
+  float t[kMaxC];     // target
+  bool in;
+};
+
+template <bool BORDER>
+__device__ __forceinline__ void stage_load(Px& p, const float* __restrict__ srcb,
+                                           const float* __restrict__ tgtb,
+                                           const float* __restrict__ mb,
+                                           const float* __restrict__ fb, int py, int px, int H,
+                                           int W, int C) {
   const int HW = H * W;
-  const int p = py * W + px;
-  tp = make_tap(fb[p], fb[HW + p], px, py, H, W, border);
-  const float wnw = tp.s * tp.e, wne = tp.s * tp.w, wsw = tp.n * tp.e, wse = tp.n * tp.w;
+  p.in = py >= 0 && px >= 0 && py < H && px < W;
+  const int cy = min(max(py, 0), H - 1), cx = min(max(px, 0), W - 1);
+  const int o = cy * W + cx;
+  p.tp = make_tap(fb[o], fb[HW + o], cx, cy, H, W, BORDER);
+  p.m = mb[o];
 #pragma unroll
   for (int c = 0; c < kMaxC; ++c) {
     if (c >= C) break;
     const float* sc = srcb + (size_t)c * HW;
-    const float vnw = tp.m_nw ? sc[tp.o_nw] : 0.f;
-    const float vne = tp.m_ne ? sc[tp.o_ne] : 0.f;
-    const float vsw = tp.m_sw ? sc[tp.o_sw] : 0.f;
-    const float vse = tp.m_se ? sc[tp.o_se] : 0.f;
-    out[c] = vnw * wnw + vne * wne + vsw * wsw + vse * wse;  // ATen's order
+    p.v[c][0] = sc[p.tp.o_nw];
+    p.v[c][1] = sc[p.tp.o_ne];
+    p.v[c][2] = sc[p.tp.o_sw];
+    p.v[c][3] = sc[p.tp.o_se];
+    p.t[c] = tgtb[(size_t)c * HW + o];
   }
 }
 
-// tile and sample of this workgroup: grid = (tiles, B), XCD-aware order so that
-// neighbouring tiles (shared halos and gather footprints) run on one L2
-__device__ __forceinline__ void photo_work(int tiles_x, int& ty0, int& tx0, int& b) {
-  const int ntiles = gridDim.x;
-  const int w = xcd_remap(linear_block(), ntiles * gridDim.y);
-  const int tile = w % ntiles;
-  b = w / ntiles;
-  ty0 = (tile / tiles_x) * kTile;
-  tx0 = (tile % tiles_x) * kTile;
+// masks applied after the loads landed; rec in ATen's order; x, y to LDS
+__device__ __forceinline__ void stage_finish(Px& p, int C, float (*xs)[kRH][kXS],
+                                             float (*ys)[kRH][kXS], int ry, int rx,
+                                             float (&rec)[kMaxC]) {
+#pragma clang fp contract(off)
+  const Tap& tp = p.tp;
+  const float wnw = tp.s * tp.e, wne = tp.s * tp.w, wsw = tp.n * tp.e, wse = tp.n * tp.w;
+#pragma unroll
+  for (int c = 0; c < kMaxC; ++c) {
+    if (c >= C) break;
+    p.v[c][0] = tp.m_nw ? p.v[c][0] : 0.f;
+    p.v[c][1] = tp.m_ne ? p.v[c][1] : 0.f;
+    p.v[c][2] = tp.m_sw ? p.v[c][2] : 0.f;
+    p.v[c][3] = tp.m_se ? p.v[c][3] : 0.f;
+    rec[c] = p.v[c][0] * wnw + p.v[c][1] * wne + p.v[c][2] * wsw + p.v[c][3] * wse;
+    xs[c][ry][rx] = p.in ? rec[c] * p.m : 0.f;
+    ys[c][ry][rx] = p.in ? p.t[c] * p.m : 0.f;
+  }
 }
 
-// block-wide sum of 3 values in a fixed order (deterministic)
+// deterministic block sum of 3 values: wave butterflies, then waves in order
 __device__ __forceinline__ void block_sum3(float a, float b, float c, float* red, float* out3) {
-  const int t = threadIdx.x;
-  red[t] = a;
-  red[256 + t] = b;
-  red[512 + t] = c;
+#pragma unroll
+  for (int s = 32; s > 0; s >>= 1) {
+    a += __shfl_xor(a, s);
+    b += __shfl_xor(b, s);
+    c += __shfl_xor(c, s);
+  }
+  const int t = threadIdx.x, wv = t >> 6;
+  if ((t & 63) == 0) {
+    red[3 * wv] = a;
+    red[3 * wv + 1] = b;
+    red[3 * wv + 2] = c;
+  }
   __syncthreads();
-  for (int s = 128; s > 0; s >>= 1) {
-    if (t < s) {
-      red[t] += red[t + s];
-      red[256 + t] += red[256 + t + s];
-      red[512 + t] += red[512 + t + s];
-    }
-    __syncthreads();
-  }
   if (t == 0) {
-    out3[0] = red[0];
-    out3[1] = red[256];
-    out3[2] = red[512];
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int w = 0; w < kNT / 64; ++w) {
+      s0 += red[3 * w];
+      s1 += red[3 * w + 1];
+      s2 += red[3 * w + 2];
+    }
+    out3[0] = s0;
+    out3[1] = s1;
+    out3[2] = s2;
   }
+}
+
+// sums over 3 columns of one region row: {x, y, x^2, y^2, xy}
+struct Row5 {
+  float sx, sy, sxx, syy, sxy;
+};
+__device__ __forceinline__ Row5 row5(const float* xr, const float* yr) {
+  Row5 r;
+  const float a0 = xr[0], a1 = xr[1], a2 = xr[2], b0 = yr[0], b1 = yr[1], b2 = yr[2];
+  r.sx = a0 + a1 + a2;
+  r.sy = b0 + b1 + b2;
+  r.sxx = fmaf(a2, a2, fmaf(a1, a1, a0 * a0));
+  r.syy = fmaf(b2, b2, fmaf(b1, b1, b0 * b0));
+  r.sxy = fmaf(a2, b2, fmaf(a1, b1, a0 * b0));
+  return r;
+}
+
+// SSIM of one window from its three row sums; with GRAD also the coefficients
+// of dS/dx_p = alpha + beta x_p + gamma y_p (zero where the clamp is active:
+// torch.clamp passes the gradient for 0 <= raw <= 1):
+//   A1 = 2 mx my + C1, A2 = 2 sig_xy + C2, B1 = mx^2 + my^2 + C1, B2 = sig_x + sig_y + C2,
+//   dS/dx_p = -(1 / (9 d)) [ my (A2 - A1) - r mx (B2 - B1) + A1 y_p - r B1 x_p ],  r = n / d
+template <bool GRAD>
+__device__ __forceinline__ float ssim_window(const Row5& r0, const Row5& r1, const Row5& r2,
+                                             float& al, float& be, float& ga) {
+  constexpr float k9 = 1.0f / 9.0f;
+  const float mx = (r0.sx + r1.sx + r2.sx) * k9, my = (r0.sy + r1.sy + r2.sy) * k9;
+  const float exx = (r0.sxx + r1.sxx + r2.sxx) * k9, eyy = (r0.syy + r1.syy + r2.syy) * k9;
+  const float exy = (r0.sxy + r1.sxy + r2.sxy) * k9;
+  const float mxy = mx * my, mx2 = mx * mx, my2 = my * my;
+  const float A1 = 2.f * mxy + kC1, A2 = 2.f * (exy - mxy) + kC2;
+  const float B1 = mx2 + my2 + kC1, B2 = (exx - mx2) + (eyy - my2) + kC2;
+  const float d = B1 * B2;
+  const float rd = __builtin_amdgcn_rcpf(d);
+  const float r = (A1 * A2) * rd;
+  const float raw = 0.5f - 0.5f * r;
+  if constexpr (GRAD) {
+    al = be = ga = 0.f;
+    if (raw >= 0.f && raw <= 1.f) {
+      const float k = -k9 * rd;
+      al = k * (my * (A2 - A1) - r * mx * (B2 - B1));
+      be = k * (-r * B1);
+      ga = k * A1;
+    }
+  }
+  return fminf(fmaxf(raw, 0.f), 1.f);
 }
 
 // ---------------------------------------------------------------- forward --
-template <bool BORDER>
-__global__ __launch_bounds__(256) void photo_fwd_kernel(const float* __restrict__ src,
-                                                        const float* __restrict__ tgt,
-                                                        const float* __restrict__ mask,
-                                                        const float* __restrict__ flow, long long fbs,
-                                                        float* __restrict__ partials, int C, int H,
-                                                        int W, int tiles_x) {
-#pragma clang fp contract(off)
-  constexpr int R = kTile + 2;  // windows starting in the tile read 2 more rows / cols
-  __shared__ float xs[kMaxC][R][R + 1], ys[kMaxC][R][R + 1];
-  __shared__ float red[768];
+// grid = (tiles, B, ndir); XCD-aware order so that neighbouring tiles (shared
+// halos and gather footprints) of one sample run on one L2
+template <bool BORDER, bool GRAD>
+__global__ __launch_bounds__(kNT) void photo_fwd_kernel(PhotoArgs a, float* __restrict__ partials) {
+  __shared__ float xs[kMaxC][kRH][kXS], ys[kMaxC][kRH][kXS];
+  __shared__ float al[GRAD ? kMaxC : 1][GRAD ? kWH : 1][GRAD ? kAS : 1];
+  __shared__ float be[GRAD ? kMaxC : 1][GRAD ? kWH : 1][GRAD ? kAS : 1];
+  __shared__ float ga[GRAD ? kMaxC : 1][GRAD ? kWH : 1][GRAD ? kAS : 1];
+  __shared__ float red[3 * kNT / 64];
   const int t = threadIdx.x;
-  int ty0, tx0, b;
-  photo_work(tiles_x, ty0, tx0, b);
-  const int HW = H * W;
-  const float* srcb = src + (size_t)b * C * HW;
-  const float* tgtb = tgt + (size_t)b * C * HW;
-  const float* mb = mask + (size_t)b * HW;
-  const float* fb = flow + b * fbs;
+  const int ntiles = gridDim.x;
+  const int w = xcd_remap(linear_block(), ntiles * gridDim.y * gridDim.z);
+  const int tile = w % ntiles;
+  const int bd = w / ntiles;  // dir * B + b
+  const int dirn = bd / a.B, b = bd - dirn * a.B;
+  const int ty0 = (tile / a.tiles_x) * kTH, tx0 = (tile % a.tiles_x) * kTW;
+  const PhotoDir& dr = a.dir[dirn];
+  const int C = a.C, H = a.H, W = a.W, HW = H * W;
+  const float* srcb = dr.src + (size_t)b * C * HW;
+  const float* tgtb = dr.tgt + (size_t)b * C * HW;
+  const float* mb = dr.mask + (size_t)b * HW;
+  const float* fb = dr.flow + b * a.fbs;
+
+  // ---- staging: own pixels (lx, ly0) and (lx, ly0 + 1), then one halo pixel
+  const int lx = t & (kTW - 1), ly0 = 2 * (t / kTW);
+  const bool has_halo = t < kHalo;
+  int hy = 0, hx = 0;
+  halo_coord(has_halo ? t : 0, hy, hx);
+  Px own[2], hp;
+#pragma unroll
+  for (int k = 0; k < 2; ++k)
+    stage_load<BORDER>(own[k], srcb, tgtb, mb, fb, ty0 + ly0 + k, tx0 + lx, H, W, C);
+  stage_load<BORDER>(hp, srcb, tgtb, mb, fb, ty0 - 2 + hy, tx0 - 2 + hx, H, W, C);
 
   float l1 = 0.f, msum = 0.f;
-  for (int e = t; e < R * R; e += 256) {
-    const int ry = e / R, rx = e - ry * R;
-    const int py = ty0 + ry, px = tx0 + rx;
-    float rec[kMaxC] = {};
-    float m = 0.f;
-    const bool in = py < H && px < W;
-    if (in) {
-      Tap tp;
-      sample_px(srcb, fb, px, py, H, W, C, BORDER, rec, tp);
-      m = mb[py * W + px];
-    }
-    const bool own = in && ry < kTile && rx < kTile;  // this tile's pixel: L1 + mask terms
-    if (own) msum += m;
+  // per own pixel: dI_c/d(ix), dI_c/d(iy) (before the coordinate factors), sign(rec - tgt)
+  float dix[2][kMaxC], diy[2][kMaxC], sg[2][kMaxC];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    float rec[kMaxC];
+    stage_finish(own[k], C, xs, ys, ly0 + k + 2, lx + 2, rec);
+    const Px& p = own[k];
+    if (p.in) msum += p.m;
 #pragma unroll
     for (int c = 0; c < kMaxC; ++c) {
       if (c >= C) break;
-      const float tv = in ? tgtb[(size_t)c * HW + py * W + px] : 0.f;
-      if (own) l1 += fabsf(tv - rec[c]) * m;
-      xs[c][ry][rx] = rec[c] * m;
-      ys[c][ry][rx] = tv * m;
+      if (p.in) l1 += fabsf(p.t[c] - rec[c]) * p.m;
+      if constexpr (GRAD) {
+        const float* v = p.v[c];
+        dix[k][c] = (v[1] - v[0]) * p.tp.s + (v[3] - v[2]) * p.tp.n;
+        diy[k][c] = (v[2] - v[0]) * p.tp.e + (v[3] - v[1]) * p.tp.w;
+        const float diff = rec[c] - p.t[c];
+        sg[k][c] = diff > 0.f ? 1.f : (diff < 0.f ? -1.f : 0.f);
+      }
     }
+  }
+  if (has_halo) {
+    float rec[kMaxC];
+    stage_finish(hp, C, xs, ys, hy, hx, rec);
   }
   __syncthreads();
-  // the 3x3 window whose top-left is this thread's pixel
+
+  // ---- windows, column-wise: item (g, wx) evaluates windows (kWG g + r, wx),
+  // r < kWG, from kWG + 2 horizontal row sums. Without GRAD only the tile's
+  // own windows (window rows / cols >= 2) are needed.
   float ssim = 0.f;
-  const int wy = t / kTile, wx = t % kTile;
-  const int qy = ty0 + wy, qx = tx0 + wx;
-  if (qy <= H - 3 && qx <= W - 3) {
+  if (t < kWItems) {
+    const int g = t / kWW, wx = t - g * kWW;
+    const int wy0 = kWG * g;
+    const int qx = tx0 - 2 + wx;
+    const bool col_ok = qx >= 0 && qx <= W - 3;
+    const bool col_own = wx >= 2;
+    if (GRAD || (col_own && wy0 + kWG > 2)) {
 #pragma unroll
-    for (int c = 0; c < kMaxC; ++c) {
-      if (c >= C) break;
-      float sx = 0.f, sy = 0.f, sxx = 0.f, syy = 0.f, sxy = 0.f;
+      for (int c = 0; c < kMaxC; ++c) {
+        if (c >= C) break;
+        Row5 rs[kWG + 2];
 #pragma unroll
-      for (int i = 0; i < 3; ++i)
+        for (int i = 0; i < kWG + 2; ++i) rs[i] = row5(&xs[c][wy0 + i][wx], &ys[c][wy0 + i][wx]);
 #pragma unroll
-        for (int j = 0; j < 3; ++j) {
-          const float a = xs[c][wy + i][wx + j], v = ys[c][wy + i][wx + j];
-          sx += a;
-          sy += v;
-          sxx += a * a;
-          syy += v * v;
-          sxy += a * v;
+        for (int r = 0; r < kWG; ++r) {
+          const int wy = wy0 + r, qy = ty0 - 2 + wy;
+          const bool valid = col_ok && qy >= 0 && qy <= H - 3;
+          float a1 = 0.f, b1 = 0.f, g1 = 0.f;
+          const float s = ssim_window<GRAD>(rs[r], rs[r + 1], rs[r + 2], a1, b1, g1);
+          if (valid && col_own && wy >= 2) ssim += s;
+          if constexpr (GRAD) {
+            al[c][wy][wx] = valid ? a1 : 0.f;
+            be[c][wy][wx] = valid ? b1 : 0.f;
+            ga[c][wy][wx] = valid ? g1 : 0.f;
+          }
         }
-      const float mx = sx / 9.f, my = sy / 9.f;
-      const float mxy = mx * my, mx2 = mx * mx, my2 = my * my;
-      const float sig_x = sxx / 9.f - mx2, sig_y = syy / 9.f - my2, sig_xy = sxy / 9.f - mxy;
-      const float n = (2.f * mxy + kC1) * (2.f * sig_xy + kC2);
-      const float d = (mx2 + my2 + kC1) * (sig_x + sig_y + kC2);
-      ssim += fminf(fmaxf((1.f - n / d) / 2.f, 0.f), 1.f);
+      }
     }
   }
-  const int blk = b * gridDim.x + (ty0 / kTile) * tiles_x + tx0 / kTile;  // fixed slot per tile
-  block_sum3(l1, ssim, msum, red, partials + 3 * blk);
+  const int blk = bd * ntiles + tile;  // fixed slot per (direction, sample, tile)
+  block_sum3(l1, ssim, msum, red, partials + 3 * blk);  // (its barrier also orders al/be/ga)
+  if constexpr (!GRAD) return;
+
+  // ---- gradient basis of the own pixels: box sums of the 9 windows around each;
+  // the two pixels share 2 of their 3 window rows (window rows ly0 .. ly0 + 3)
+  float ax[2] = {0.f, 0.f}, ay[2] = {0.f, 0.f}, bx[2] = {0.f, 0.f}, by[2] = {0.f, 0.f};
+#pragma unroll
+  for (int c = 0; c < kMaxC; ++c) {
+    if (c >= C) break;
+    float ra[4], rb[4], rg[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float* pa = &al[c][ly0 + i][lx];
+      const float* pb = &be[c][ly0 + i][lx];
+      const float* pg = &ga[c][ly0 + i][lx];
+      ra[i] = pa[0] + pa[1] + pa[2];
+      rb[i] = pb[0] + pb[1] + pb[2];
+      rg[i] = pg[0] + pg[1] + pg[2];
+    }
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const float sa = ra[k] + ra[k + 1] + ra[k + 2];
+      const float sb = rb[k] + rb[k + 1] + rb[k + 2];
+      const float sgm = rg[k] + rg[k + 1] + rg[k + 2];
+      const float xp = xs[c][ly0 + k + 2][lx + 2], yp = ys[c][ly0 + k + 2][lx + 2];
+      const float ds = sa + sb * xp + sgm * yp;  // sum_q dS_q / dx_pc
+      ax[k] += sg[k][c] * dix[k][c];
+      ay[k] += sg[k][c] * diy[k][c];
+      bx[k] += ds * dix[k][c];
+      by[k] += ds * diy[k][c];
+    }
+  }
+  // dL/drec_pc carries the mask m (x = rec m); grid grad -> norm_grid autograd
+  const float fxs = 2.0f / (float)(W - 1), fys = 2.0f / (float)(H - 1);
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const Px& p = own[k];
+    if (!p.in) continue;
+    const float kx = p.m * p.tp.mx * fxs, ky = p.m * p.tp.my * fys;
+    float* o = dr.basis + (size_t)b * a.bbs + (ty0 + ly0 + k) * W + tx0 + lx;
+    o[0] = ax[k] * kx;
+    o[HW] = ay[k] * ky;
+    o[2 * HW] = bx[k] * kx;
+    o[3 * HW] = by[k] * ky;
+  }
 }
 
-// One block: fixed-order fp64 sum of the partials -> out = {loss, c_l1, c_ssim}
-// with c_* the backward coefficients w_* / (N_* * (mean(m) + 1e-6)).
-__global__ __launch_bounds__(256) void photo_final_kernel(const float* __restrict__ partials,
-                                                          int nblk, float* __restrict__ out,
-                                                          double n1, double n2, double n3, float w_l1,
-                                                          float w_ssim) {
-  __shared__ double red[3][256];
-  const int t = threadIdx.x;
+// One block per direction: fixed-order fp64 sum of its partials ->
+// out[3 dir ..] = {loss, c_l1, c_ssim}, c_* = w_* / (N_* * (mean(m) + 1e-6)).
+constexpr int kFinNT = 512;
+__global__ __launch_bounds__(kFinNT) void photo_final_kernel(const float* __restrict__ partials,
+                                                             int nblk, float* __restrict__ out,
+                                                             double n1, double n2, double n3,
+                                                             float w_l1, float w_ssim) {
+  __shared__ double red[3][kFinNT / 64];
+  const int t = threadIdx.x, dirn = blockIdx.x;
+  const float* p = partials + (size_t)3 * nblk * dirn;
   double a = 0, b = 0, c = 0;
-  for (int i = t; i < nblk; i += 256) {
-    a += partials[3 * i];
-    b += partials[3 * i + 1];
-    c += partials[3 * i + 2];
-  }
-  red[0][t] = a;
-  red[1][t] = b;
-  red[2][t] = c;
-  __syncthreads();
-  for (int s = 128; s > 0; s >>= 1) {
-    if (t < s) {
-      red[0][t] += red[0][t + s];
-      red[1][t] += red[1][t + s];
-      red[2][t] += red[2][t + s];
+  int i = t;
+  // 4 slots in flight per thread, summed in slot order (fixed)
+  for (; i + 3 * kFinNT < nblk; i += 4 * kFinNT) {
+    float v[4][3];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int q = 0; q < 3; ++q) v[j][q] = p[3 * (i + j * kFinNT) + q];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      a += v[j][0];
+      b += v[j][1];
+      c += v[j][2];
     }
-    __syncthreads();
   }
+  for (; i < nblk; i += kFinNT) {
+    a += p[3 * i];
+    b += p[3 * i + 1];
+    c += p[3 * i + 2];
+  }
+#pragma unroll
+  for (int s = 32; s > 0; s >>= 1) {
+    a += __shfl_xor(a, s);
+    b += __shfl_xor(b, s);
+    c += __shfl_xor(c, s);
+  }
+  if ((t & 63) == 0) {
+    red[0][t >> 6] = a;
+    red[1][t >> 6] = b;
+    red[2][t >> 6] = c;
+  }
+  __syncthreads();
   if (t == 0) {
-    const double den = red[2][0] / n3 + 1e-6;
-    const double l1 = n1 > 0 ? red[0][0] / n1 : 0.0, ss = n2 > 0 ? red[1][0] / n2 : 0.0;
-    out[0] = (float)((w_l1 * l1 + w_ssim * ss) / den);
-    out[1] = n1 > 0 ? (float)(w_l1 / (n1 * den)) : 0.f;
-    out[2] = n2 > 0 ? (float)(w_ssim / (n2 * den)) : 0.f;
+    double s0 = 0, s1 = 0, s2 = 0;
+    for (int w = 0; w < kFinNT / 64; ++w) {
+      s0 += red[0][w];
+      s1 += red[1][w];
+      s2 += red[2][w];
+    }
+    const double den = s2 / n3 + 1e-6;
+    const double l1 = n1 > 0 ? s0 / n1 : 0.0, ss = n2 > 0 ? s1 / n2 : 0.0;
+    float* o = out + 3 * dirn;
+    o[0] = (float)((w_l1 * l1 + w_ssim * ss) / den);
+    o[1] = n1 > 0 ? (float)(w_l1 / (n1 * den)) : 0.f;
+    o[2] = n2 > 0 ? (float)(w_ssim / (n2 * den)) : 0.f;
   }
 }
 
 // --------------------------------------------------------------- backward --
-// d S_q / d x_p for a pixel p of window q (x = rec * m, y = tgt * m):
-//   A1 = 2 mx my + C1, A2 = 2 sig_xy + C2, B1 = mx^2 + my^2 + C1, B2 = sig_x + sig_y + C2,
-//   n = A1 A2, d = B1 B2, r = n / d, S = (1 - r) / 2 (clamped to [0, 1]):
-//   dS/dx_p = -(1 / (9 d)) [ my (A2 - A1) - r mx (B2 - B1) + A1 y_p - r B1 x_p ]
-//           = alpha + beta x_p + gamma y_p,  zero where the clamp is active
-//   (torch.clamp passes the gradient for 0 <= raw <= 1).
-template <bool BORDER>
-__global__ __launch_bounds__(256) void photo_bwd_kernel(const float* __restrict__ src,
-                                                        const float* __restrict__ tgt,
-                                                        const float* __restrict__ mask,
-                                                        const float* __restrict__ flow, long long fbs,
+// gflow[b, 2 dir + j, p] = g_dir (c_l1 basis[b, 4 dir + j, p] + c_ssim basis[b, 4 dir + 2 + j, p])
+__global__ __launch_bounds__(256) void photo_bwd_kernel(const float* __restrict__ basis,
                                                         const float* __restrict__ coef,
                                                         const float* __restrict__ gloss,
-                                                        float* __restrict__ gflow, int C, int H,
-                                                        int W, int tiles_x) {
-#pragma clang fp contract(off)
-  constexpr int RI = kTile + 4;  // x / y region: rows ty0-2 .. ty0+TH+1
-  constexpr int RW = kTile + 2;  // windows: top-left rows ty0-2 .. ty0+TH-1
-  __shared__ float xs[kMaxC][RI][RI + 1], ys[kMaxC][RI][RI + 1];
-  __shared__ float al[kMaxC][RW][RW + 1], be[kMaxC][RW][RW + 1], ga[kMaxC][RW][RW + 1];
-  __shared__ float corners[kMaxC][4][kTile * kTile];  // own pixels' source corners
-  const int t = threadIdx.x;
-  int ty0, tx0, b;
-  photo_work(tiles_x, ty0, tx0, b);
-  const int HW = H * W;
-  const float* srcb = src + (size_t)b * C * HW;
-  const float* tgtb = tgt + (size_t)b * C * HW;
-  const float* mb = mask + (size_t)b * HW;
-  const float* fb = flow + b * fbs;
+                                                        float* __restrict__ gflow, int HW, int ndir) {
+  const int dirn = blockIdx.z, b = blockIdx.y;
+  const float gl = gloss[dirn];
+  const float k1 = coef[3 * dirn + 1] * gl, k2 = coef[3 * dirn + 2] * gl;
+  const float* a = basis + ((size_t)b * ndir + dirn) * 4 * HW;
+  float* o = gflow + ((size_t)b * ndir + dirn) * 2 * HW;
+  const int i = (blockIdx.x * 256 + threadIdx.x) * 4;
+  if ((HW & 3) == 0) {
+    if (i >= HW) return;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const float4 u = *reinterpret_cast<const float4*>(a + j * HW + i);
+      const float4 v = *reinterpret_cast<const float4*>(a + (2 + j) * HW + i);
+      *reinterpret_cast<float4*>(o + j * HW + i) =
+          make_float4(k1 * u.x + k2 * v.x, k1 * u.y + k2 * v.y, k1 * u.z + k2 * v.z, k1 * u.w + k2 * v.w);
+    }
+  } else {
+    for (int e = i; e < i + 4 && e < HW; ++e)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) o[j * HW + e] = k1 * a[j * HW + e] + k2 * a[(2 + j) * HW + e];
+  }
+}
 
-  for (int e = t; e < RI * RI; e += 256) {
-    const int ry = e / RI, rx = e - ry * RI;
-    const int py = ty0 - 2 + ry, px = tx0 - 2 + rx;
-    float m = 0.f;
-    const bool in = py >= 0 && px >= 0 && py < H && px < W;
-    const bool own = ry >= 2 && rx >= 2 && ry < kTile + 2 && rx < kTile + 2;
-    const int o = (ry - 2) * kTile + (rx - 2);
-    Tap tp;
-    if (in) {
-      tp = make_tap(fb[py * W + px], fb[HW + py * W + px], px, py, H, W, BORDER);
-      m = mb[py * W + px];
-    }
-    // one channel at a time: gather the 4 corners, keep them in LDS for the
-    // owned pixels (the coordinate derivative below needs them), store x and y
-#pragma unroll
-    for (int c = 0; c < kMaxC; ++c) {
-      if (c >= C) break;
-      float v0 = 0.f, v1 = 0.f, v2 = 0.f, v3 = 0.f, r = 0.f;
-      if (in) {
-        const float* sc = srcb + (size_t)c * HW;
-        v0 = tp.m_nw ? sc[tp.o_nw] : 0.f;
-        v1 = tp.m_ne ? sc[tp.o_ne] : 0.f;
-        v2 = tp.m_sw ? sc[tp.o_sw] : 0.f;
-        v3 = tp.m_se ? sc[tp.o_se] : 0.f;
-        r = v0 * (tp.s * tp.e) + v1 * (tp.s * tp.w) + v2 * (tp.n * tp.e) + v3 * (tp.n * tp.w);
-      }
-      xs[c][ry][rx] = r * m;
-      ys[c][ry][rx] = in ? tgtb[(size_t)c * HW + py * W + px] * m : 0.f;
-      if (own) {
-        corners[c][0][o] = v0;
-        corners[c][1][o] = v1;
-        corners[c][2][o] = v2;
-        corners[c][3][o] = v3;
-      }
-    }
+hipError_t photo_launch(const PhotoArgs& a, int ndir, int pad_mode, float* partials, float* out,
+                        float w_l1, float w_ssim, hipStream_t s) {
+  const int tiles_y = (a.H + kTH - 1) / kTH;
+  const int ntiles = a.tiles_x * tiles_y;
+  const dim3 grid((unsigned)ntiles, (unsigned)a.B, (unsigned)ndir);
+  const bool grad = a.dir[0].basis != nullptr;
+  if (pad_mode == 1) {
+    if (grad)
+      hipLaunchKernelGGL((photo_fwd_kernel<true, true>), grid, dim3(kNT), 0, s, a, partials);
+    else
+      hipLaunchKernelGGL((photo_fwd_kernel<true, false>), grid, dim3(kNT), 0, s, a, partials);
+  } else {
+    if (grad)
+      hipLaunchKernelGGL((photo_fwd_kernel<false, true>), grid, dim3(kNT), 0, s, a, partials);
+    else
+      hipLaunchKernelGGL((photo_fwd_kernel<false, false>), grid, dim3(kNT), 0, s, a, partials);
   }
-  __syncthreads();
-  for (int e = t; e < RW * RW; e += 256) {
-    const int wy = e / RW, wx = e - wy * RW;
-    const int qy = ty0 - 2 + wy, qx = tx0 - 2 + wx;
-    const bool valid = qy >= 0 && qx >= 0 && qy <= H - 3 && qx <= W - 3;
-#pragma unroll
-    for (int c = 0; c < kMaxC; ++c) {
-      if (c >= C) break;
-      float a = 0.f, bb = 0.f, g = 0.f;
-      if (valid) {
-        float sx = 0.f, sy = 0.f, sxx = 0.f, syy = 0.f, sxy = 0.f;
-#pragma unroll
-        for (int i = 0; i < 3; ++i)
-#pragma unroll
-          for (int j = 0; j < 3; ++j) {
-            const float u = xs[c][wy + i][wx + j], v = ys[c][wy + i][wx + j];
-            sx += u;
-            sy += v;
-            sxx += u * u;
-            syy += v * v;
-            sxy += u * v;
-          }
-        const float mx = sx / 9.f, my = sy / 9.f;
-        const float mxy = mx * my, mx2 = mx * mx, my2 = my * my;
-        const float sig_x = sxx / 9.f - mx2, sig_y = syy / 9.f - my2, sig_xy = sxy / 9.f - mxy;
-        const float A1 = 2.f * mxy + kC1, A2 = 2.f * sig_xy + kC2;
-        const float B1 = mx2 + my2 + kC1, B2 = sig_x + sig_y + kC2;
-        const float n = A1 * A2, d = B1 * B2;
-        const float r = n / d;
-        const float raw = (1.f - r) / 2.f;
-        if (raw >= 0.f && raw <= 1.f) {
-          const float k = -1.f / (9.f * d);
-          a = k * (my * (A2 - A1) - r * mx * (B2 - B1));
-          bb = k * (-r * B1);
-          g = k * A1;
-        }
-      }
-      al[c][wy][wx] = a;
-      be[c][wy][wx] = bb;
-      ga[c][wy][wx] = g;
-    }
-  }
-  __syncthreads();
-  const int ly = t / kTile, lx = t % kTile;
-  const int py = ty0 + ly, px = tx0 + lx;
-  if (py >= H || px >= W) return;
-  const float gl = *gloss;
-  const float c_l1 = coef[1] * gl, c_ss = coef[2] * gl;
-  const int HWp = py * W + px;
-  const Tap tp = make_tap(fb[HWp], fb[HW + HWp], px, py, H, W, BORDER);  // weights + masks only
-  const float m = mb[HWp];
-  float dix = 0.f, diy = 0.f;
-#pragma unroll
-  for (int c = 0; c < kMaxC; ++c) {
-    if (c >= C) break;
-    // windows covering p have top-left (py - i, px - j), i, j in 0..2 -> local (ly + 2 - i, lx + 2 - j)
-    float sa = 0.f, sb = 0.f, sg = 0.f;
-#pragma unroll
-    for (int i = 0; i < 3; ++i)
-#pragma unroll
-      for (int j = 0; j < 3; ++j) {
-        sa += al[c][ly + 2 - i][lx + 2 - j];
-        sb += be[c][ly + 2 - i][lx + 2 - j];
-        sg += ga[c][ly + 2 - i][lx + 2 - j];
-      }
-    const float xp = xs[c][ly + 2][lx + 2], yp = ys[c][ly + 2][lx + 2];
-    const float tv = tgtb[(size_t)c * HW + py * W + px];
-    const float vnw = corners[c][0][t], vne = corners[c][1][t];
-    const float vsw = corners[c][2][t], vse = corners[c][3][t];
-    const float rec = vnw * (tp.s * tp.e) + vne * (tp.s * tp.w) + vsw * (tp.n * tp.e) + vse * (tp.n * tp.w);
-    const float diff = rec - tv;
-    const float sgn = diff > 0.f ? 1.f : (diff < 0.f ? -1.f : 0.f);
-    const float g = (c_l1 * sgn + c_ss * (sa + sb * xp + sg * yp)) * m;  // dL / d rec_c
-    dix += ((vne - vnw) * tp.s + (vse - vsw) * tp.n) * g;
-    diy += ((vsw - vnw) * tp.e + (vse - vne) * tp.w) * g;
-  }
-  // grid grad, then norm_grid's autograd (warp.hip, warp_bwd_kernel)
-  const float ggx = dix * tp.mx, ggy = diy * tp.my;
-  float* gf = gflow + (size_t)b * 2 * HW + py * W + px;
-  gf[0] = (ggx / (float)(W - 1)) * 2.0f;
-  gf[HW] = (ggy / (float)(H - 1)) * 2.0f;
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const double n1 = (double)a.B * a.C * a.H * a.W;
+  const double n2 = (a.H >= 3 && a.W >= 3) ? (double)a.B * a.C * (a.H - 2) * (a.W - 2) : 0.0;
+  const double n3 = (double)a.B * a.H * a.W;
+  hipLaunchKernelGGL(photo_final_kernel, dim3((unsigned)ndir), dim3(kFinNT), 0, s, partials,
+                     ntiles * a.B, out, n1, n2, n3, w_l1, w_ssim);
+  return hipGetLastError();
 }
 
 }  // namespace
 
 int photo_partials(int B, int H, int W) {
-  return 3 * B * ((H + kTile - 1) / kTile) * ((W + kTile - 1) / kTile);
+  return 3 * B * ((H + kTH - 1) / kTH) * ((W + kTW - 1) / kTW);
 }
 
 hipError_t photo_fwd_launch(const float* src, const float* tgt, const float* mask, const float* flow,
-                            long long fbs, float* partials, float* out, int B, int C, int H, int W,
-                            int pad_mode, float w_l1, float w_ssim, hipStream_t s) {
-  const int tiles_x = (W + kTile - 1) / kTile, tiles_y = (H + kTile - 1) / kTile;
-  const dim3 grid((unsigned)(tiles_x * tiles_y), (unsigned)B);
-  if (pad_mode == 1)
-    hipLaunchKernelGGL(photo_fwd_kernel<true>, grid, dim3(256), 0, s, src, tgt, mask, flow, fbs,
-                       partials, C, H, W, tiles_x);
-  else
-    hipLaunchKernelGGL(photo_fwd_kernel<false>, grid, dim3(256), 0, s, src, tgt, mask, flow, fbs,
-                       partials, C, H, W, tiles_x);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return e;
-  const double n1 = (double)B * C * H * W;
-  const double n2 = (H >= 3 && W >= 3) ? (double)B * C * (H - 2) * (W - 2) : 0.0;
-  const double n3 = (double)B * H * W;
-  hipLaunchKernelGGL(photo_final_kernel, dim3(1), dim3(256), 0, s, partials, tiles_x * tiles_y * B,
-                     out, n1, n2, n3, w_l1, w_ssim);
-  return hipGetLastError();
+                            long long fbs, float* partials, float* out, float* basis, int B, int C,
+                            int H, int W, int pad_mode, float w_l1, float w_ssim, hipStream_t s) {
+  PhotoArgs a{};
+  a.dir[0] = PhotoDir{src, tgt, mask, flow, basis};
+  a.dir[1] = a.dir[0];
+  a.fbs = fbs;
+  a.bbs = 4LL * H * W;
+  a.B = B; a.C = C; a.H = H; a.W = W;
+  a.tiles_x = (W + kTW - 1) / kTW;
+  return photo_launch(a, 1, pad_mode, partials, out, w_l1, w_ssim, s);
 }
 
-hipError_t photo_bwd_launch(const float* src, const float* tgt, const float* mask, const float* flow,
-                            long long fbs, const float* coef, const float* gloss, float* gflow,
-                            int B, int C, int H, int W, int pad_mode, hipStream_t s) {
-  const int tiles_x = (W + kTile - 1) / kTile, tiles_y = (H + kTile - 1) / kTile;
-  const dim3 grid((unsigned)(tiles_x * tiles_y), (unsigned)B);
-  if (pad_mode == 1)
-    hipLaunchKernelGGL(photo_bwd_kernel<true>, grid, dim3(256), 0, s, src, tgt, mask, flow, fbs,
-                       coef, gloss, gflow, C, H, W, tiles_x);
-  else
-    hipLaunchKernelGGL(photo_bwd_kernel<false>, grid, dim3(256), 0, s, src, tgt, mask, flow, fbs,
-                       coef, gloss, gflow, C, H, W, tiles_x);
+// both directions of a with_bk scale: dir 0 warps im2 by flow[:, 0:2] onto im1
+// (mask1), dir 1 warps im1 by flow[:, 2:4] onto im2 (mask2) (flow_loss.py:130-131).
+// basis: [B, 2, 4, H, W] (= [B,8,H,W]) or null.
+hipError_t photo_pair_fwd_launch(const float* im1, const float* im2, const float* mask1,
+                                 const float* mask2, const float* flow, long long fbs,
+                                 float* partials, float* out, float* basis, int B, int C, int H,
+                                 int W, int pad_mode, float w_l1, float w_ssim, hipStream_t s) {
+  PhotoArgs a{};
+  const size_t HW = (size_t)H * W;
+  // basis block of (sample b, direction d) at basis + (2 b + d) * 4HW
+  a.dir[0] = PhotoDir{im2, im1, mask1, flow, basis};
+  a.dir[1] = PhotoDir{im1, im2, mask2, flow + 2 * HW, basis ? basis + 4 * HW : nullptr};
+  a.fbs = fbs;
+  a.bbs = 8LL * H * W;
+  a.B = B; a.C = C; a.H = H; a.W = W;
+  a.tiles_x = (W + kTW - 1) / kTW;
+  return photo_launch(a, 2, pad_mode, partials, out, w_l1, w_ssim, s);
+}
+
+hipError_t photo_bwd_launch(const float* basis, const float* coef, const float* gloss, float* gflow,
+                            int B, int H, int W, int ndir, hipStream_t s) {
+  const int HW = H * W;
+  const dim3 grid((unsigned)((HW + 1023) / 1024), (unsigned)B, (unsigned)ndir);
+  hipLaunchKernelGGL(photo_bwd_kernel, grid, dim3(256), 0, s, basis, coef, gloss, gflow, HW, ndir);
   return hipGetLastError();
 }
 

@@ -75,11 +75,14 @@ hipError_t occ_backward_launch(const float* flow, long long flow_bstride, float*
 
 int photo_partials(int B, int H, int W);
 hipError_t photo_fwd_launch(const float* src, const float* tgt, const float* mask, const float* flow,
-                            long long flow_bstride, float* partials, float* out, int B, int C, int H,
-                            int W, int pad_mode, float w_l1, float w_ssim, hipStream_t s);
-hipError_t photo_bwd_launch(const float* src, const float* tgt, const float* mask, const float* flow,
-                            long long flow_bstride, const float* coef, const float* gloss,
-                            float* gflow, int B, int C, int H, int W, int pad_mode, hipStream_t s);
+                            long long flow_bstride, float* partials, float* out, float* basis, int B,
+                            int C, int H, int W, int pad_mode, float w_l1, float w_ssim, hipStream_t s);
+hipError_t photo_pair_fwd_launch(const float* im1, const float* im2, const float* mask1,
+                                 const float* mask2, const float* flow, long long flow_bstride,
+                                 float* partials, float* out, float* basis, int B, int C, int H,
+                                 int W, int pad_mode, float w_l1, float w_ssim, hipStream_t s);
+hipError_t photo_bwd_launch(const float* basis, const float* coef, const float* gloss, float* gflow,
+                            int B, int H, int W, int ndir, hipStream_t s);
 
 hipError_t upsample_fwd_launch(const float* x, float* out, int B, int C, int H, int W, int k,
                                hipStream_t s);

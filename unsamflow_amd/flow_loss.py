@@ -171,12 +171,13 @@ class unFlowLoss(nn.Module):  # noqa: N801 (reference name)
                     m1 = torch.ones((b, 1, h, w), dtype=torch.float32, device=dev)
                     m2 = torch.ones((b, 1, h, w), dtype=torch.float32, device=dev)
                 if self._fused_photometric(flow):
-                    from .photometric import photometric_loss
+                    from .photometric import photometric_loss, photometric_loss_pair
 
-                    lw = photometric_loss(flow[:, :2], im2_s, im1_s, m1, c.warp_pad, c.w_l1, c.w_ssim)
-                    if c.with_bk:
-                        lw = (lw + photometric_loss(flow[:, 2:], im1_s, im2_s, m2, c.warp_pad, c.w_l1,
-                                                    c.w_ssim)) / 2.0
+                    if c.with_bk:  # both directions in one launch
+                        lp = photometric_loss_pair(flow, im1_s, im2_s, m1, m2, c.warp_pad, c.w_l1, c.w_ssim)
+                        lw = (lp[0] + lp[1]) / 2.0
+                    else:
+                        lw = photometric_loss(flow[:, :2], im2_s, im1_s, m1, c.warp_pad, c.w_l1, c.w_ssim)
                 else:
                     im1_rec = self.warp(im2_s, flow[:, :2], pad=c.warp_pad)
                     im2_rec = self.warp(im1_s, flow[:, 2:], pad=c.warp_pad)

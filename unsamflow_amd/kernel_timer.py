@@ -161,7 +161,13 @@ def site_launcher(op: str, key, device, seed: int = 0):
             return lambda: ops.flow_upsample(f, k)
         go = torch.randn(B, C, H * k, W * k, device=device, generator=g)
         return lambda: ops.flow_upsample_backward(go, k)
-    if op in ("occ_bwd", "splat", "photo_fwd", "photo_bwd"):
+    if op == "photo_bwd":
+        B, ndir, H, W = key
+        basis = torch.randn(B, 4 * ndir, H, W, device=device, generator=g)
+        coef = torch.rand(3 * ndir, device=device, generator=g)
+        gl = torch.ones(ndir, device=device)
+        return lambda: ops.photo_loss_backward(basis, coef, gl)
+    if op in ("occ_bwd", "splat", "photo_fwd", "photo_fwd_grad", "photo_pair", "photo_pair_grad"):
         B, C, H, W = key[:4]
         yy = torch.linspace(0, 6.2832, H, device=device).view(1, 1, H, 1)
         xx = torch.linspace(0, 6.2832, W, device=device).view(1, 1, 1, W)
@@ -175,11 +181,12 @@ def site_launcher(op: str, key, device, seed: int = 0):
         src = torch.rand(B, C, H, W, device=device, generator=g)
         tgt = torch.rand(B, C, H, W, device=device, generator=g)
         mask = (torch.rand(B, 1, H, W, device=device, generator=g) > 0.1).float()
-        if op == "photo_fwd":
-            return lambda: ops.photo_loss_forward(src, tgt, mask, flow, pad)
-        coef = ops.photo_loss_forward(src, tgt, mask, flow, pad)
-        gl = torch.ones(1, device=device)
-        return lambda: ops.photo_loss_backward(src, tgt, mask, flow, coef, gl, pad)
+        if op.startswith("photo_pair"):
+            flow4 = torch.cat([flow, -flow], 1)
+            mask2 = mask.flip(-1).contiguous()
+            return lambda: ops.photo_loss_pair_forward(flow4, tgt, src, mask, mask2, pad,
+                                                       need_grad=op == "photo_pair_grad")
+        return lambda: ops.photo_loss_forward(src, tgt, mask, flow, pad, need_grad=op == "photo_fwd_grad")
     B, C, H, W, pad = key[:5]
     x = torch.rand(B, C, H, W, device=device, generator=g)
     yy = torch.linspace(0, 6.2832, H, device=device).view(1, 1, H, 1)

@@ -237,41 +237,93 @@ def _photo_args(src, tgt, mask, flow):
         raise ValueError(f"tgt {tuple(tgt.shape)} / mask {tuple(mask.shape)} do not match src {(B, C, H, W)}")
     if C > 3:
         raise NotImplementedError(f"fused photometric loss supports C <= 3 image channels, got {C}")
+    if flow is None:
+        return src.contiguous(), tgt.contiguous(), mask.contiguous(), B, C, H, W
     _require_device_f32("flow", flow)
     fv, fbs = _flow_view(flow, B, H, W)
     return src.contiguous(), tgt.contiguous(), mask.contiguous(), fv, fbs, B, C, H, W
 
 
-def photo_loss_forward(src, tgt, mask, flow, pad: str = "border", w_l1: float = 0.15, w_ssim: float = 0.85):
+def photo_loss_forward(src, tgt, mask, flow, pad: str = "border", w_l1: float = 0.15, w_ssim: float = 0.85,
+                       need_grad: bool = False):
     """Fused warp + occlusion-aware L1/SSIM photometric loss of one scale and
-    direction (flow_loss.py:127-148, loss_blocks.py:53-72) -> tensor [3] on the
-    device: {loss, c_l1, c_ssim} (the last two feed the backward)."""
+    direction (flow_loss.py:127-148, loss_blocks.py:53-72) -> (out, basis):
+    ``out`` = tensor [3] on the device {loss, c_l1, c_ssim}; with ``need_grad``
+    ``basis`` = [B,4,H,W], the per-pixel flow-gradient basis computed in the
+    same pass (dL/dflow = c_l1 * basis[:, :2] + c_ssim * basis[:, 2:]), else None."""
     if pad not in PAD_MODES:
         raise NotImplementedError(f"flow_warp padding mode {pad!r} (supported: border, zeros)")
     s, t, m, fv, fbs, B, C, H, W = _photo_args(src, tgt, mask, flow)
     lib = _lib.load()
     partials = torch.empty(lib.usf_photo_loss_partials(B, H, W), device=src.device, dtype=torch.float32)
     out = torch.empty(3, device=src.device, dtype=torch.float32)
-    with torch.cuda.device(src.device), _kt.timed("photo_fwd", (B, C, H, W, pad), src.device,
-                                                    4 * B * H * W * (2 * C + 3)):
+    basis = torch.empty((B, 4, H, W), device=src.device, dtype=torch.float32) if need_grad else None
+    # algorithmic bytes: src, tgt, mask, flow read once; the basis written once
+    nbytes = 4 * B * H * W * (2 * C + 3 + (4 if need_grad else 0))
+    op = "photo_fwd_grad" if need_grad else "photo_fwd"
+    with torch.cuda.device(src.device), _kt.timed(op, (B, C, H, W, pad), src.device, nbytes):
         rc = lib.usf_photo_loss_fwd_f32(s.data_ptr(), t.data_ptr(), m.data_ptr(), fv.data_ptr(), fbs,
-                                        partials.data_ptr(), out.data_ptr(), B, C, H, W, PAD_MODES[pad],
-                                        float(w_l1), float(w_ssim), _lib.stream_handle(src.device))
+                                        partials.data_ptr(), out.data_ptr(),
+                                        basis.data_ptr() if need_grad else None, B, C, H, W,
+                                        PAD_MODES[pad], float(w_l1), float(w_ssim),
+                                        _lib.stream_handle(src.device))
     _lib.check(rc, "usf_photo_loss_fwd_f32")
-    return out
+    return out, basis
 
 
-def photo_loss_backward(src, tgt, mask, flow, coef, grad_loss, pad: str = "border"):
-    """d(photo loss)/d(flow) * grad_loss -> [B,2,H,W] (deterministic)."""
-    s, t, m, fv, fbs, B, C, H, W = _photo_args(src, tgt, mask, flow)
-    gl = grad_loss.reshape(1).to(torch.float32).contiguous()
-    gflow = torch.empty((B, 2, H, W), device=src.device, dtype=torch.float32)
+def photo_loss_pair_forward(flow, im1, im2, mask1, mask2, pad: str = "border", w_l1: float = 0.15,
+                            w_ssim: float = 0.85, need_grad: bool = False):
+    """Both directions of a with_bk scale in one launch (flow_loss.py:130-131):
+    direction 0 = loss(im1, warp(im2, flow[:, :2]), mask1), direction 1 =
+    loss(im2, warp(im1, flow[:, 2:]), mask2) -> (out [6] = {loss, c_l1, c_ssim}
+    per direction, basis [B,8,H,W] (= [B,2,4,H,W]) or None)."""
+    if pad not in PAD_MODES:
+        raise NotImplementedError(f"flow_warp padding mode {pad!r} (supported: border, zeros)")
+    a, b_, m1, B, C, H, W = _photo_args(im1, im2, mask1, None)
+    m2 = mask2.contiguous()
+    _require_device_f32("mask2", m2)
+    if tuple(m2.shape) != (B, 1, H, W):
+        raise ValueError(f"mask2 {tuple(m2.shape)} does not match {(B, 1, H, W)}")
+    _require_device_f32("flow", flow)
+    if tuple(flow.shape) != (B, 4, H, W):
+        raise ValueError(f"flow must be [B,4,H,W] = {(B, 4, H, W)}, got {tuple(flow.shape)}")
+    fv = flow if flow[0].is_contiguous() else flow.contiguous()
+    fbs = fv.stride(0) if B > 1 else 4 * H * W
     lib = _lib.load()
-    with torch.cuda.device(src.device), _kt.timed("photo_bwd", (B, C, H, W, pad), src.device,
-                                                    4 * B * H * W * (2 * C + 5)):
-        rc = lib.usf_photo_loss_bwd_f32(s.data_ptr(), t.data_ptr(), m.data_ptr(), fv.data_ptr(), fbs,
-                                        coef.data_ptr(), gl.data_ptr(), gflow.data_ptr(), B, C, H, W,
-                                        PAD_MODES[pad], _lib.stream_handle(src.device))
+    partials = torch.empty(2 * lib.usf_photo_loss_partials(B, H, W), device=im1.device, dtype=torch.float32)
+    out = torch.empty(6, device=im1.device, dtype=torch.float32)
+    basis = torch.empty((B, 8, H, W), device=im1.device, dtype=torch.float32) if need_grad else None
+    nbytes = 2 * 4 * B * H * W * (2 * C + 3 + (4 if need_grad else 0))
+    op = "photo_pair_grad" if need_grad else "photo_pair"
+    with torch.cuda.device(im1.device), _kt.timed(op, (B, C, H, W, pad), im1.device, nbytes):
+        rc = lib.usf_photo_loss_pair_fwd_f32(a.data_ptr(), b_.data_ptr(), m1.data_ptr(), m2.data_ptr(),
+                                             fv.data_ptr(), fbs, partials.data_ptr(), out.data_ptr(),
+                                             basis.data_ptr() if need_grad else None, B, C, H, W,
+                                             PAD_MODES[pad], float(w_l1), float(w_ssim),
+                                             _lib.stream_handle(im1.device))
+    _lib.check(rc, "usf_photo_loss_pair_fwd_f32")
+    return out, basis
+
+
+def photo_loss_backward(basis, coef, grad_loss):
+    """d(photo loss)/d(flow) * grad_loss from the forward's gradient basis
+    ([B,4,H,W] one direction, [B,8,H,W] a pair) and coefficients ->
+    [B,2,H,W] / [B,4,H,W] (deterministic)."""
+    _require_device_f32("basis", basis)
+    B, K, H, W = _nchw("basis", basis)
+    if K not in (4, 8):
+        raise ValueError(f"gradient basis must be [B,4,H,W] or [B,8,H,W], got {tuple(basis.shape)}")
+    ndir = K // 4
+    basis = basis.contiguous()
+    gl = grad_loss.reshape(-1).to(torch.float32).contiguous()
+    if gl.numel() != ndir:
+        raise ValueError(f"grad_loss has {gl.numel()} elements for {ndir} direction(s)")
+    gflow = torch.empty((B, 2 * ndir, H, W), device=basis.device, dtype=torch.float32)
+    lib = _lib.load()
+    with torch.cuda.device(basis.device), _kt.timed("photo_bwd", (B, ndir, H, W), basis.device,
+                                                      4 * B * H * W * 6 * ndir):
+        rc = lib.usf_photo_loss_bwd_f32(basis.data_ptr(), coef.data_ptr(), gl.data_ptr(), gflow.data_ptr(),
+                                        B, H, W, ndir, _lib.stream_handle(basis.device))
     _lib.check(rc, "usf_photo_loss_bwd_f32")
     return gflow
 

@@ -1,9 +1,11 @@
 """Fused photometric loss: the per-scale, per-direction
 ``loss_photomatric(im1_s, flow_warp(im2_s, flow), vis_mask)`` of
 losses/flow_loss.py:127-148 (L1 + SSIM, loss_blocks.py:53-72) as one autograd
-op over two HIP kernels (unsamflow_amd/csrc/photo.hip): no warped image, SSIM
-maps or intermediate gradients in HBM, and the gradient reaches only the flow
-(the images and the thresholded occlusion mask carry none, as in the reference).
+op (unsamflow_amd/csrc/photo.hip): no warped image, SSIM maps or intermediate
+gradients in HBM, and the gradient reaches only the flow (the images and the
+thresholded occlusion mask carry none, as in the reference). When the flow needs
+a gradient, the forward pass also writes the per-pixel gradient basis (the loss
+is linear in its L1 and SSIM sums), so the backward is one dense pass.
 """
 from __future__ import annotations
 
@@ -16,17 +18,18 @@ from . import ops
 class PhotometricLossFunction(Function):
     @staticmethod
     def forward(ctx, flow, src, tgt, mask, pad, w_l1, w_ssim):
-        out = ops.photo_loss_forward(src, tgt, mask, flow, pad, w_l1, w_ssim)
-        ctx.save_for_backward(flow, src, tgt, mask, out)
-        ctx.pad = pad
+        need = ctx.needs_input_grad[0]
+        out, basis = ops.photo_loss_forward(src, tgt, mask, flow, pad, w_l1, w_ssim, need_grad=need)
+        if need:
+            ctx.save_for_backward(basis, out)
         return out[0].clone()
 
     @staticmethod
     def backward(ctx, grad_loss):
-        flow, src, tgt, mask, out = ctx.saved_tensors
         gflow = None
         if ctx.needs_input_grad[0]:
-            gflow = ops.photo_loss_backward(src, tgt, mask, flow, out, grad_loss, ctx.pad)
+            basis, out = ctx.saved_tensors
+            gflow = ops.photo_loss_backward(basis, out, grad_loss)
         return gflow, None, None, None, None, None, None
 
 
@@ -36,3 +39,38 @@ def photometric_loss(flow: torch.Tensor, src: torch.Tensor, tgt: torch.Tensor, m
     if src.requires_grad or tgt.requires_grad:
         raise NotImplementedError("the fused photometric loss differentiates w.r.t. the flow only")
     return PhotometricLossFunction.apply(flow, src, tgt, mask.detach(), pad, float(w_l1), float(w_ssim))
+
+
+class PhotometricPairFunction(Function):
+    """Both directions of a with_bk scale in one launch: returns [2] losses
+    (direction 0: im1 vs warp(im2, flow[:, :2]) under mask1; direction 1: im2
+    vs warp(im1, flow[:, 2:]) under mask2); the gradient is [B,4,H,W]."""
+
+    @staticmethod
+    def forward(ctx, flow, im1, im2, mask1, mask2, pad, w_l1, w_ssim):
+        need = ctx.needs_input_grad[0]
+        out, basis = ops.photo_loss_pair_forward(flow, im1, im2, mask1, mask2, pad, w_l1, w_ssim,
+                                                 need_grad=need)
+        if need:
+            ctx.save_for_backward(basis, out)
+        return out.view(2, 3)[:, 0].clone()
+
+    @staticmethod
+    def backward(ctx, grad_losses):
+        gflow = None
+        if ctx.needs_input_grad[0]:
+            basis, out = ctx.saved_tensors
+            gflow = ops.photo_loss_backward(basis, out, grad_losses)
+        return gflow, None, None, None, None, None, None, None
+
+
+def photometric_loss_pair(flow: torch.Tensor, im1: torch.Tensor, im2: torch.Tensor, mask1: torch.Tensor,
+                          mask2: torch.Tensor, pad: str = "border", w_l1: float = 0.15,
+                          w_ssim: float = 0.85) -> torch.Tensor:
+    """``[loss_photomatric(im1, flow_warp(im2, flow[:, :2]), mask1),
+    loss_photomatric(im2, flow_warp(im1, flow[:, 2:]), mask2)]`` (flow_loss.py:130-131)
+    in one launch; ``flow`` is the [B,4,H,W] forward+backward flow."""
+    if im1.requires_grad or im2.requires_grad:
+        raise NotImplementedError("the fused photometric loss differentiates w.r.t. the flow only")
+    return PhotometricPairFunction.apply(flow, im1, im2, mask1.detach(), mask2.detach(), pad, float(w_l1),
+                                         float(w_ssim))
