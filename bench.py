@@ -70,6 +70,9 @@ def parse():
                     help="skip the graph-replay device times (keeps a rocprofv3 run to real steps only)")
     ap.add_argument("--cudnn-benchmark", action="store_true",
                     help="MIOpen find-mode tuning of the convolutions (slow first steps)")
+    ap.add_argument("--graph", action="store_true",
+                    help="replay the step from HIP graphs (harness.GraphedTrainStep); measured equal to "
+                         "eager at N=1 (the step is GPU-bound), so eager is the default")
     return ap.parse_args()
 
 
@@ -243,31 +246,55 @@ def main():
     torch.backends.cudnn.benchmark = bool(args.cudnn_benchmark)
 
     from unsamflow_amd import _lib
-    from unsamflow_amd.harness import TrainStep, synthetic_pair
+    from unsamflow_amd.harness import GraphedTrainStep, TrainStep, broadcast_params, synthetic_pair
     from unsamflow_amd.kernel_timer import KernelTimer
 
     _lib.load()  # fail loudly if the HIP library is missing
     c = CONFIGS[args.config]
     cfg = cfg_for(args.config)
-    step = TrainStep(cfg, device, ddp=distributed, seed=42 + rank)
+    use_graph = args.graph
+    # graph mode: the whole step is captured once and replayed (harness.GraphedTrainStep);
+    # data parallel = one all-reduce of the flat gradient buffer between the two graphs
+    step = TrainStep(cfg, device, ddp=distributed and not use_graph, seed=42 + rank, capturable=use_graph)
     img1, img2, s1, s2 = synthetic_pair(args.batch, c["H"], c["W"], device, seed=42 + rank,
                                         with_seg=args.config != "kitti")
 
-    for i in range(args.warmup):
-        step(img1, img2, s1, s2)
+    if use_graph:
+        if distributed:
+            broadcast_params(step.module)
+        gstep = GraphedTrainStep(step, img1, img2, s1, s2, warmup=max(3, args.warmup))
+        for _ in range(2):
+            gstep()
+        run = gstep
+    else:
+        for i in range(args.warmup):
+            step(img1, img2, s1, s2)
+        run = lambda: step(img1, img2, s1, s2)  # noqa: E731
     torch.cuda.synchronize()
 
     if distributed:
         dist.barrier()
     torch.cuda.synchronize()
-    with KernelTimer() as kt:  # two event records per hot-path launch, no syncs
+    # eager: two event records per hot-path launch inside the timed region (no syncs);
+    # graph replays carry no host code, so their per-site times come from the
+    # in-step pass below
+    with KernelTimer(enabled=not use_graph) as kt:
         t0 = time.perf_counter()
         for _ in range(args.steps):
-            loss = step(img1, img2, s1, s2)
+            loss = run()
         torch.cuda.synchronize()
     if distributed:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    if use_graph:
+        # per-site kernel times: the same step run eagerly for K steps with HIP
+        # events around every library launch (kernel durations do not depend on
+        # how the launch was issued; rocprofv3 of the replays cross-checks them)
+        torch.cuda.synchronize()
+        with KernelTimer() as kt:
+            for _ in range(args.steps):
+                step(img1, img2, s1, s2)
+            torch.cuda.synchronize()
     if distributed:
         t = torch.tensor([elapsed], device=device, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -304,6 +331,7 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic U[0,1) frame pairs, random-init PWCLite weights",
+            "execution": "hip-graph replay of the captured step" if use_graph else "eager",
             "config": {
                 "workload": c["workload"],
                 "global_batch": args.batch * world,

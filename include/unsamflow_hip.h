@@ -26,6 +26,8 @@
  *                        caller losses/flow_loss.py:101-103 (occ_from_back)
  *   usf_photo_loss_*  <- the per-scale warp + loss_photomatric composition of
  *                        losses/flow_loss.py:127-148
+ *   usf_area_pyramid  <- the loss's per-scale F.interpolate(im, mode="area")
+ *                        (losses/flow_loss.py:118-125)
  *   usf_flow_upsample_* <- F.interpolate(flow * k, scale_factor=k, bilinear,
  *                        align_corners=True) of the decoder (pwclite.py:299-301;
  *                        SURVEY §8f row 4)
@@ -97,10 +99,17 @@ int usf_corr_bwd_f32(const float* x1, const float* x2, const float* gout,
 /* usf_corr_fwd_f32 writing into a channel slice of a larger buffer (the flow
  * estimator's concat input, pwclite.py:364-366): sample b's (2d+1)^2 output
  * planes start at out + b * out_bstride (elements; planes H*W apart), and
- * act = USF_ACT_LEAKY_RELU applies v > 0 ? v : v * slope to every output. */
+ * act = USF_ACT_LEAKY_RELU applies v > 0 ? v : v * slope to every output.
+ * workspace (nullable, caller-provided device scratch of workspace_floats
+ * floats): when it holds usf_corr_fwd_workspace(B,C,H,W,d) floats, small
+ * levels split the channel loop over more workgroups and reduce the partials
+ * in a fixed order (deterministic); otherwise the unsplit kernel runs. */
 int usf_corr_fwd_ex_f32(const float* x1, const float* x2, float* out, long long out_bstride,
-                        int act, float slope, int B, int C, int H, int W, int d,
-                        void* stream);
+                        int act, float slope, float* workspace, long long workspace_floats,
+                        int B, int C, int H, int W, int d, void* stream);
+
+/* Floats of workspace usf_corr_fwd_ex_f32 uses at this shape (0: no split). */
+long long usf_corr_fwd_workspace(int B, int C, int H, int W, int d);
 
 /* usf_corr_bwd_f32 reading its gradient from a channel slice (batch stride
  * g_bstride, elements). With act_out != NULL (the forward's activated output,
@@ -195,6 +204,14 @@ int usf_flow_upsample_f32(const float* flow, float* out, int B, int C, int H, in
  * from grad_out [B,C,H*factor,W*factor]. */
 int usf_flow_upsample_bwd_f32(const float* grad_out, float* grad_flow, int B, int C, int H,
                               int W, int factor, void* stream);
+
+/* The loss's image pyramid (unFlowLoss per scale s: F.interpolate(im,
+ * (H >> s, W >> s), mode="area"), flow_loss.py:118-125): out_s = mean of each
+ * 2^s x 2^s block, summed in row-major order as torch's CPU kernel does
+ * (bit-exact). x: [B,C,H,W] dense with H % 8 == 0 and W % 8 == 0; out1/2/3:
+ * [B,C,H/2,W/2], [B,C,H/4,W/4], [B,C,H/8,W/8] dense, overwritten. */
+int usf_area_pyramid_f32(const float* x, float* out1, float* out2, float* out3, int B, int C,
+                         int H, int W, void* stream);
 
 /* Tuning hook (benchmarking only; not needed for correct use).
  * Forces kernel variant `index` of `op` for d=4 launches in this process:

@@ -72,3 +72,51 @@ def test_ddp_two_ranks_gloo(tmp_path):
         assert torch.equal(a, b)
         torch.testing.assert_close(a, (l0 + l1) / 2, atol=1e-7, rtol=1e-5)
     assert any(not torch.equal(l0, l1) for l0, l1 in zip(r0["local"], r1["local"]))
+
+
+def _flat_worker(rank, world, port, out_dir):
+    """The graphed multi-GPU step's exchange (harness.FlatGrads): parameters
+    broadcast from rank 0, local backward into the flat gradient buffer, ONE
+    all-reduce of that buffer, mean -> equals DDP's averaged gradient; then
+    clip + Adam keep the replicas identical."""
+    sys.path.insert(0, REPO)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.set_num_threads(2)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from oracle.hashrng import hash_init_
+    from oracle.torch_ref import OracleCorrelation, oracle_flow_warp, oracle_occu_mask_backward
+    from unsamflow_amd.config import kitti_base
+    from unsamflow_amd.harness import FlatGrads, TrainStep, broadcast_params, synthetic_pair
+
+    cfg = kitti_base()
+    step = TrainStep(cfg, "cpu", corr_module=OracleCorrelation(4), warp_fn=oracle_flow_warp,
+                     occ_backward_fn=oracle_occu_mask_backward, seed=7 + rank)
+    hash_init_(step.module, seed=3 + rank)  # replicas differ until the broadcast
+    broadcast_params(step.module)
+    img1, img2, _, _ = synthetic_pair(1, 64, 128, "cpu", seed=100 + rank)
+    grads = FlatGrads(step.module.parameters())
+    for _ in range(2):  # the buffer is re-zeroed each step (no stale accumulation)
+        grads.zero_()
+        loss, _ = step.forward_loss(img1, img2)
+        loss.backward()
+    local = grads.flat.clone()
+    grads.all_reduce_mean()
+    torch.save({"local": local, "mean": grads.flat.clone()}, os.path.join(out_dir, f"flat{rank}.pt"))
+    torch.nn.utils.clip_grad_norm_(grads.params, step.max_grad_norm)
+    step.optimizer.step()
+    flat = torch.cat([p.detach().reshape(-1) for p in step.module.parameters()])
+    gathered = [torch.zeros_like(flat) for _ in range(world)]
+    dist.all_gather(gathered, flat)
+    assert torch.equal(gathered[0], gathered[1])
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(600)
+def test_flat_gradient_allreduce_two_ranks_gloo(tmp_path):
+    world = 2
+    mp.spawn(_flat_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    r0 = torch.load(tmp_path / "flat0.pt", weights_only=True)
+    r1 = torch.load(tmp_path / "flat1.pt", weights_only=True)
+    assert torch.equal(r0["mean"], r1["mean"])
+    torch.testing.assert_close(r0["mean"], (r0["local"] + r1["local"]) / 2, atol=1e-7, rtol=1e-5)
+    assert not torch.equal(r0["local"], r1["local"])

@@ -414,3 +414,31 @@ def test_occlusion_vs_oracle_full_size(hip_device, shape, scale):
     np.testing.assert_allclose(absm, cmap_ref, atol=2e-6, rtol=1e-6)
     # mass conservation: every in-image target spreads exactly its weights
     assert abs(float(rel.sum()) - float(cmap_ref.sum())) < 1e-3 * max(1.0, float(cmap_ref.sum()))
+
+
+@pytest.mark.parametrize("shape", [(8, 192, 4, 13), (8, 128, 8, 26), (8, 96, 16, 52), (3, 100, 5, 9)])
+def test_corr_fwd_channel_split_vs_unsplit_and_oracle(hip_device, shape):
+    """Small levels split the forward's channel loop (usf_corr_fwd_workspace > 0):
+    the fixed-order reduction of the group partials matches the unsplit kernel
+    (usf_corr_fwd_f32, no workspace) and the fp64 oracle; with the LeakyReLU
+    epilogue into a concat slice it matches the composition."""
+    from unsamflow_amd import _lib, ops
+
+    B, C, H, W = shape
+    lib = _lib.load()
+    assert lib.usf_corr_fwd_workspace(B, C, H, W, 4) > 0
+    x1 = hashrng.normal(shape, 5 + C)
+    x2 = hashrng.normal(shape, 6 + C)
+    t1, t2 = _dev(x1, hip_device), _dev(x2, hip_device)
+    split = ops.corr_forward(t1, t2, 4)
+    plain = torch.empty_like(split)
+    rc = lib.usf_corr_fwd_f32(t1.data_ptr(), t2.data_ptr(), plain.data_ptr(), B, C, H, W, 4,
+                              _lib.stream_handle(t1.device))
+    _lib.check(rc, "usf_corr_fwd_f32")
+    ref = corr_forward_np(x1, x2, 4)
+    np.testing.assert_allclose(_np(split), ref, atol=CORR_ATOL, rtol=CORR_RTOL)
+    np.testing.assert_allclose(_np(split), _np(plain), atol=2e-6, rtol=1e-5)
+    cat = torch.full((B, 81 + 7, H, W), 7.0, device=hip_device)
+    ops.corr_forward_ex(t1, t2, 4, cat[:, 3:84], leaky_slope=0.1)
+    np.testing.assert_allclose(_np(cat[:, 3:84]), _np(torch.nn.functional.leaky_relu(split, 0.1)), atol=0, rtol=0)
+    assert float(cat[:, :3].min()) == 7.0 and float(cat[:, 84:].max()) == 7.0

@@ -26,3 +26,19 @@ def test_flow_upsample_matches_torch(hip_device, shape, k):
     out.backward(go.to(hip_device))
     np.testing.assert_allclose(out.detach().cpu().numpy(), ref.detach().numpy(), atol=2e-5, rtol=1e-6)
     np.testing.assert_allclose(fd.grad.cpu().numpy(), fr.grad.numpy(), atol=2e-4, rtol=1e-5)
+
+
+@pytest.mark.parametrize("B,C,H,W", [(2, 3, 256, 832), (1, 3, 448, 1024), (3, 1, 8, 16), (2, 3, 24, 40)])
+def test_area_pyramid_bit_exact_vs_torch_cpu(hip_device, B, C, H, W):
+    """usf_area_pyramid_f32 == F.interpolate(x, (H >> s, W >> s), mode="area")
+    on the CPU (torch's row-major block sum, / k / k), bit for bit."""
+    import torch.nn.functional as F
+
+    from oracle import hashrng
+    from unsamflow_amd import ops
+
+    x = torch.from_numpy(hashrng.uniform((B, C, H, W), 77 + H))
+    outs = ops.area_pyramid(x.to(hip_device))
+    for s, o in zip((1, 2, 3), outs):
+        ref = F.interpolate(x, (H >> s, W >> s), mode="area")
+        assert torch.equal(o.cpu(), ref), (s, float((o.cpu() - ref).abs().max()))

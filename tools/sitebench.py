@@ -37,6 +37,8 @@ def site_list(ops):
             out += [(op, (8, 2, H, W)) for H, W in SCALES]
         elif op == "occ_bwd":
             out += [(op, (8, 1, 256, 832))]
+        elif op == "area_pyramid":
+            out += [(op, (8, 3, 256, 832))]
         else:
             raise SystemExit(f"unknown op {op}")
     return out
@@ -65,6 +67,8 @@ def alg_bytes(op, key):
         return 2 * 4 * B * H * W * (2 * C + 7)
     if op == "occ_bwd":
         return 4 * B * H * W * 3
+    if op == "area_pyramid":
+        return int(4 * B * C * H * W * (1 + 1 / 4 + 1 / 16 + 1 / 64))
     raise KeyError(op)
 
 

@@ -35,9 +35,11 @@ _SIGNATURES = {
         ctypes.c_int,
     ),
     "usf_corr_fwd_ex_f32": (
-        [_c_float_p] * 3 + [ctypes.c_longlong, ctypes.c_int, ctypes.c_float] + [ctypes.c_int] * 5 + [ctypes.c_void_p],
+        [_c_float_p] * 3 + [ctypes.c_longlong, ctypes.c_int, ctypes.c_float, _c_float_p, ctypes.c_longlong]
+        + [ctypes.c_int] * 5 + [ctypes.c_void_p],
         ctypes.c_int,
     ),
+    "usf_corr_fwd_workspace": ([ctypes.c_int] * 5, ctypes.c_longlong),
     "usf_corr_bwd_ex_f32": (
         [_c_float_p] * 3 + [ctypes.c_longlong, _c_float_p, ctypes.c_float] + [_c_float_p] * 3
         + [ctypes.c_int] * 5 + [ctypes.c_void_p],
@@ -78,6 +80,7 @@ _SIGNATURES = {
     ),
     "usf_flow_upsample_f32": ([_c_float_p] * 2 + [ctypes.c_int] * 5 + [ctypes.c_void_p], ctypes.c_int),
     "usf_flow_upsample_bwd_f32": ([_c_float_p] * 2 + [ctypes.c_int] * 5 + [ctypes.c_void_p], ctypes.c_int),
+    "usf_area_pyramid_f32": ([_c_float_p] * 4 + [ctypes.c_int] * 4 + [ctypes.c_void_p], ctypes.c_int),
     "usf_set_variant": ([ctypes.c_int, ctypes.c_int], ctypes.c_int),
 }
 EXPORTED_SYMBOLS = tuple(_SIGNATURES)

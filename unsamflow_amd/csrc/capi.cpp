@@ -104,8 +104,14 @@ int usf_corr_fwd_f32(const float* x1, const float* x2, float* out, int B, int C,
                 (hipStream_t)stream);
 }
 
+long long usf_corr_fwd_workspace(int B, int C, int H, int W, int d) {
+  if (B <= 0 || C <= 0 || H <= 0 || W <= 0 || d < 1 || d > 4) return 0;
+  return corr_fwd_workspace(B, C, H, W, d);
+}
+
 int usf_corr_fwd_ex_f32(const float* x1, const float* x2, float* out, long long out_bstride,
-                        int act, float slope, int B, int C, int H, int W, int d, void* stream) {
+                        int act, float slope, float* workspace, long long workspace_floats, int B,
+                        int C, int H, int W, int d, void* stream) {
   clear_error();
   if (!check_dims("usf_corr_fwd_ex_f32", B, C, H, W)) return USF_EINVAL;
   if (d < 1 || d > 4) {
@@ -128,7 +134,7 @@ int usf_corr_fwd_ex_f32(const float* x1, const float* x2, float* out, long long 
   if (const int pe = pre_check("usf_corr_fwd_ex_f32", (hipStream_t)stream)) return pe;
   return finish("usf_corr_fwd_ex_f32",
                 corr_fwd_launch(x1, x2, out, B, C, H, W, d, (hipStream_t)stream,
-                                FwdEpi{out_bstride, act, slope}),
+                                FwdEpi{out_bstride, act, slope}, workspace, workspace_floats),
                 (hipStream_t)stream);
 }
 
@@ -391,6 +397,24 @@ int usf_flow_upsample_bwd_f32(const float* grad_out, float* grad_flow, int B, in
   if (const int pe = pre_check("usf_flow_upsample_bwd_f32", (hipStream_t)stream)) return pe;
   return finish("usf_flow_upsample_bwd_f32",
                 upsample_bwd_launch(grad_out, grad_flow, B, C, H, W, factor, (hipStream_t)stream),
+                (hipStream_t)stream);
+}
+
+int usf_area_pyramid_f32(const float* x, float* out1, float* out2, float* out3, int B, int C, int H,
+                         int W, void* stream) {
+  clear_error();
+  const char* fn = "usf_area_pyramid_f32";
+  if (!check_dims(fn, B, C, H, W)) return USF_EINVAL;
+  if (H % 8 != 0 || W % 8 != 0) {
+    set_error("%s: H=%d and W=%d must be multiples of 8", fn, H, W);
+    return USF_EINVAL;
+  }
+  if (!x || !out1 || !out2 || !out3) {
+    set_error("%s: null pointer", fn);
+    return USF_EINVAL;
+  }
+  if (const int pe = pre_check(fn, (hipStream_t)stream)) return pe;
+  return finish(fn, area_pyramid_launch(x, out1, out2, out3, (long long)B * C, H, W, (hipStream_t)stream),
                 (hipStream_t)stream);
 }
 

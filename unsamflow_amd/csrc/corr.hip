@@ -32,6 +32,7 @@
 //    in VGPRs for the whole channel loop (g read once per workgroup); per
 //    channel the DYW partial rows are summed in registers, the NW per-wave
 //    partials are added through LDS in a fixed order and written once.
+#include <algorithm>
 #include <cstdint>
 
 #include "usf_common.h"
@@ -289,11 +290,16 @@ __global__ __launch_bounds__(64 * NDY) void corr_fwd_kernel(const float* __restr
   USF_TRACE_HWID();
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  // work item: displacement-row group fastest, then tile, then sample
+  // work item: displacement-row group fastest, then tile, then (sample, channel group)
   const int w = xcd_remap(linear_block(), gridDim.x * gridDim.y * gridDim.z);
   const int dyb = (w % F::NDYG) * NDY;
   const int tile = (w / F::NDYG) % gridDim.y;
-  const int b = w / (F::NDYG * gridDim.y);
+  const int bz = w / (F::NDYG * gridDim.y);
+  const int G = ep.groups;
+  const int b = bz / G, grp = bz - b * G;
+  // channel range of this workgroup (whole C without a split)
+  const int cg = G > 1 ? round_up((C + G - 1) / G, CC) : C;
+  const int cbeg = grp * cg, cend = min(C, cbeg + cg);
   const int ty = tile / tiles_x;
   const int tx = tile - ty * tiles_x;
   const int y0 = ty * TH, x0 = tx * TW;
@@ -310,8 +316,8 @@ __global__ __launch_bounds__(64 * NDY) void corr_fwd_kernel(const float* __restr
   const rsrc_t r1 = plane_rsrc(x1 + (size_t)b * C * HW, true, C * HW * 4);
   const rsrc_t r2 = plane_rsrc(x2 + (size_t)b * C * HW, true, C * HW * 4);
   auto dma_stage = [&](int c0, float* img) {
-    s1.load(r1, img, wave, c0, C, HW);
-    s2.load(r2, img + N1, wave, c0, C, HW);
+    s1.load(r1, img, wave, c0, cend, HW);
+    s2.load(r2, img + N1, wave, c0, cend, HW);
   };
 
   float acc[K][PX];
@@ -320,14 +326,14 @@ __global__ __launch_bounds__(64 * NDY) void corr_fwd_kernel(const float* __restr
 #pragma unroll
     for (int i = 0; i < PX; ++i) acc[j][i] = 0.f;
 
-  dma_stage(0, sm);
+  dma_stage(cbeg, sm);
   dma_wait_all();
   __syncthreads();
   USF_TRACE_AT(1);
   int st = 0;
-  for (int c0 = 0; c0 < C; c0 += CC, ++st) {
+  for (int c0 = cbeg; c0 < cend; c0 += CC, ++st) {
     const float* cur = sm + (st & 1) * STAGE;
-    if (c0 + CC < C) dma_stage(c0 + CC, sm + ((st + 1) & 1) * STAGE);  // in flight during FMAs
+    if (c0 + CC < cend) dma_stage(c0 + CC, sm + ((st + 1) & 1) * STAGE);  // in flight during FMAs
     USF_TRACE_AT(2 + 4 * st);
     if (active) {
       const float* p1 = cur + r * S + q * PX;
@@ -358,6 +364,25 @@ __global__ __launch_bounds__(64 * NDY) void corr_fwd_kernel(const float* __restr
   const int y = y0 + r;
   if (y >= H) return;
   const int xb = x0 + q * PX;
+  if (G > 1) {  // raw channel-group partials [g][b][k][p]; corr_fwd_reduce_kernel finishes
+    const int Bn = gridDim.z / G;
+    float* pb = ep.part + ((size_t)(grp * Bn + b) * K * K + (size_t)dy * K) * HW + y * W + xb;
+    const bool pvec = ((W & 3) == 0) && (xb + PX <= W);
+#pragma unroll
+    for (int dx = 0; dx < K; ++dx) {
+      if (pvec) {
+#pragma unroll
+        for (int i = 0; i < PX / 4; ++i)
+          reinterpret_cast<float4*>(pb + dx * HW)[i] =
+              make_float4(acc[dx][4 * i], acc[dx][4 * i + 1], acc[dx][4 * i + 2], acc[dx][4 * i + 3]);
+      } else {
+#pragma unroll
+        for (int i = 0; i < PX; ++i)
+          if (xb + i < W) pb[dx * HW + i] = acc[dx][i];
+      }
+    }
+    return;
+  }
   const float cf = (float)C;
   // output planes of sample b start at b * ep.out_bstride (a channel slice of a
   // concat buffer, or the dense [B,K*K,H,W] tensor); LeakyReLU epilogue on request
@@ -385,15 +410,53 @@ __global__ __launch_bounds__(64 * NDY) void corr_fwd_kernel(const float* __restr
   }
 }
 
+// out[b * obs + k * HW + p] = epilogue(sum_g part[g][b][k][p] / C), g in order
+__global__ __launch_bounds__(256) void corr_fwd_reduce_kernel(const float* __restrict__ part,
+                                                              float* __restrict__ out, FwdEpi ep,
+                                                              int G, int B, int KHW, int C) {
+  const long long per = (long long)B * KHW;
+  const long long i0 = ((long long)blockIdx.x * 256 + threadIdx.x) * 4;
+  if (i0 >= per) return;
+  const float cf = (float)C;
+  auto fin = [&](float s) {
+    const float v = s / cf;
+    return ep.act ? (v > 0.f ? v : v * ep.slope) : v;
+  };
+  if ((KHW & 3) == 0 && (ep.out_bstride & 3) == 0) {
+    float4 s = *reinterpret_cast<const float4*>(part + i0);
+    for (int g = 1; g < G; ++g) {
+      const float4 v = *reinterpret_cast<const float4*>(part + g * per + i0);
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+    const long long b = i0 / KHW, r = i0 - b * KHW;
+    *reinterpret_cast<float4*>(out + b * ep.out_bstride + r) = make_float4(fin(s.x), fin(s.y), fin(s.z), fin(s.w));
+  } else {
+    for (long long i = i0; i < i0 + 4 && i < per; ++i) {
+      float s = part[i];
+      for (int g = 1; g < G; ++g) s += part[g * per + i];
+      const long long b = i / KHW, r = i - b * KHW;
+      out[b * ep.out_bstride + r] = fin(s);
+    }
+  }
+}
+
 template <int D, int PX, int SEGX, int NDY, int CC, int V>
 hipError_t launch_fwd_v(const float* x1, const float* x2, float* out, int B, int C, int H, int W,
                         hipStream_t s, FwdEpi ep) {
   using F = FwdCfg<D, PX, SEGX, NDY, CC, V>;
   const int tiles_x = (W + F::TW - 1) / F::TW;
   const int tiles_y = (H + F::TH - 1) / F::TH;
-  dim3 grid(F::NDYG, tiles_x * tiles_y, B);
+  dim3 grid(F::NDYG, tiles_x * tiles_y, B * ep.groups);
   hipLaunchKernelGGL((corr_fwd_kernel<D, PX, SEGX, NDY, CC, V>), grid, dim3(F::NT), 0, s, x1,
                      x2, out, C, H, W, tiles_x, ep);
+  if (ep.groups > 1) {
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    const int KHW = F::K * F::K * H * W;
+    const long long per = (long long)B * KHW;
+    hipLaunchKernelGGL(corr_fwd_reduce_kernel, dim3((unsigned)((per + 1023) / 1024)), dim3(256), 0, s,
+                       ep.part, out, ep, ep.groups, B, KHW, C);
+  }
   return hipGetLastError();
 }
 
@@ -425,22 +488,52 @@ hipError_t fwd_candidate_d4(int i, const float* x1, const float* x2, float* out,
 }
 constexpr int kFwdCandidates = 8;
 
+// Shape heuristic: all displacement rows in one workgroup (x1/x2 staged once)
+// when that still fills the 256 CUs; else split displacement rows across
+// workgroups (profiles/r01_v4_kbench.json: <4,8,9,4> is the fastest d=4
+// candidate at the 64x208 level, <4,8,3,8> at 32x104 and below). Small levels
+// (KITTI L0-L2: 24-96 workgroups, 12-24 serial channel stages of ~2 us DMA
+// round trip each) also split the channel loop over `groups` workgroups
+// (>= 2 stages each) when the caller provides the workspace for the partials.
+struct FwdPlan {
+  int cfg;     // 0: <4,8,K,4>, 1: <4,8,K,8>, 2: <4,8,3,8>
+  int groups;  // channel groups
+};
+template <int D>
+FwdPlan fwd_plan(int B, int C, int H, int W) {
+  constexpr int K = 2 * D + 1;
+  const long tiles32 = (long)((W + 31) / 32) * ((H + 7) / 8);
+  FwdPlan p{2, 1};
+  const long big = (long)B * ((W + 63) / 64) * ((H + 7) / 8);
+  if (big >= 256) p.cfg = 0;
+  else if ((long)B * tiles32 >= 256) p.cfg = 1;
+  if (p.cfg == 2) {
+    const long wgs = (long)B * tiles32 * ((K + 2) / 3);
+    if (wgs < 192) {
+      const int CC = 8;
+      int g = (int)((384 + wgs - 1) / wgs);
+      p.groups = std::max(1, std::min(g, C / (2 * CC)));
+    }
+  }
+  return p;
+}
+
 template <int D>
 hipError_t fwd_dispatch(const float* x1, const float* x2, float* out, int B, int C, int H,
-                        int W, hipStream_t s, FwdEpi ep) {
+                        int W, hipStream_t s, FwdEpi ep, float* ws, long long ws_floats) {
   constexpr int K = 2 * D + 1;
   if (D == 4) {
     const int forced = variant_override(0);
     if (forced >= 0) return fwd_candidate_d4(forced, x1, x2, out, B, C, H, W, s, ep);
   }
-  // All displacement rows in one workgroup (x1/x2 staged once) when that
-  // still fills the 256 CUs; else split displacement rows across workgroups.
-  // (profiles/r01_v4_kbench.json: <4,8,9,4> is the fastest d=4 candidate at
-  // the 64x208 level, <4,8,3,8> at 32x104 and below.)
-  const long big = (long)B * ((W + 63) / 64) * ((H + 7) / 8);
-  if (big >= 256) return launch_fwd<D, 4, 8, K, 4>(x1, x2, out, B, C, H, W, s, ep);
-  const long mid = (long)B * ((W + 31) / 32) * ((H + 7) / 8);
-  if (mid >= 256) return launch_fwd<D, 4, 8, K, 8>(x1, x2, out, B, C, H, W, s, ep);
+  const FwdPlan p = fwd_plan<D>(B, C, H, W);
+  if (p.cfg == 0) return launch_fwd<D, 4, 8, K, 4>(x1, x2, out, B, C, H, W, s, ep);
+  if (p.cfg == 1) return launch_fwd<D, 4, 8, K, 8>(x1, x2, out, B, C, H, W, s, ep);
+  const long long need = (long long)p.groups * B * K * K * H * W;
+  if (p.groups > 1 && ws && ws_floats >= need) {
+    ep.part = ws;
+    ep.groups = p.groups;
+  }
   return launch_fwd<D, 4, 8, 3, 8>(x1, x2, out, B, C, H, W, s, ep);
 }
 
@@ -757,14 +850,30 @@ int variant_count(int op) { return op == 0 ? kFwdCandidates : op == 1 ? kBwdCand
 void set_variant_override(int op, int index) { __atomic_store_n(&g_variant[op], index, __ATOMIC_RELAXED); }
 
 hipError_t corr_fwd_launch(const float* x1, const float* x2, float* out, int B, int C, int H,
-                           int W, int d, hipStream_t s, FwdEpi ep) {
+                           int W, int d, hipStream_t s, FwdEpi ep, float* ws, long long ws_floats) {
+  ep.part = nullptr;
+  ep.groups = 1;
   switch (d) {
-    case 1: return fwd_dispatch<1>(x1, x2, out, B, C, H, W, s, ep);
-    case 2: return fwd_dispatch<2>(x1, x2, out, B, C, H, W, s, ep);
-    case 3: return fwd_dispatch<3>(x1, x2, out, B, C, H, W, s, ep);
-    case 4: return fwd_dispatch<4>(x1, x2, out, B, C, H, W, s, ep);
+    case 1: return fwd_dispatch<1>(x1, x2, out, B, C, H, W, s, ep, ws, ws_floats);
+    case 2: return fwd_dispatch<2>(x1, x2, out, B, C, H, W, s, ep, ws, ws_floats);
+    case 3: return fwd_dispatch<3>(x1, x2, out, B, C, H, W, s, ep, ws, ws_floats);
+    case 4: return fwd_dispatch<4>(x1, x2, out, B, C, H, W, s, ep, ws, ws_floats);
     default: return hipErrorInvalidValue;
   }
+}
+
+long long corr_fwd_workspace(int B, int C, int H, int W, int d) {
+  FwdPlan p{2, 1};
+  switch (d) {
+    case 1: p = fwd_plan<1>(B, C, H, W); break;
+    case 2: p = fwd_plan<2>(B, C, H, W); break;
+    case 3: p = fwd_plan<3>(B, C, H, W); break;
+    case 4: p = fwd_plan<4>(B, C, H, W); break;
+    default: return 0;
+  }
+  if (p.groups <= 1) return 0;
+  const long long K = 2 * d + 1;
+  return (long long)p.groups * B * K * K * H * W;
 }
 
 hipError_t corr_bwd_launch(const float* x1, const float* x2, const float* gout, float* gx1,

@@ -10,6 +10,13 @@
 // 4x smaller input). Backward: deterministic gather form -- each input element
 // sums the weights of the few output rows / columns whose taps reach it
 // (ATen scatters with atomics), times k.
+//
+// Also the loss's image pyramid (flow_loss.py:118-125 of the reference's
+// unFlowLoss: F.interpolate(im, (H >> s, W >> s), mode="area") per scale s):
+// adaptive_avg_pool2d with exact 2^s blocks = the block's elements summed in
+// row-major order, then / k / k (torch's CPU order, bit-exact; the divisions
+// are by powers of two). One thread reads an 8x8 block once (16 float4 loads)
+// and writes all three coarser scales.
 #include "usf_common.h"
 
 namespace usf {
@@ -89,6 +96,52 @@ __global__ __launch_bounds__(256) void upsample_bwd_kernel(const float* __restri
   gx[i] = acc * k;
 }
 
+// planes x (H/8) x (W/8) threads; H % 8 == 0, W % 8 == 0 (checked by the caller)
+__global__ __launch_bounds__(256) void area_pyramid_kernel(const float* __restrict__ x,
+                                                           float* __restrict__ o1,
+                                                           float* __restrict__ o2,
+                                                           float* __restrict__ o3, long long planes,
+                                                           int H, int W) {
+#pragma clang fp contract(off)
+  const int bw = W >> 3, bh = H >> 3;
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= planes * bh * bw) return;
+  const int bx = (int)(i % bw);
+  const int by = (int)((i / bw) % bh);
+  const long long pl = i / ((long long)bh * bw);
+  const float* xp = x + pl * H * W + (by * 8) * W + bx * 8;
+  float v[8][8];
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+    const float4 a = reinterpret_cast<const float4*>(xp + r * W)[0];
+    const float4 b = reinterpret_cast<const float4*>(xp + r * W)[1];
+    v[r][0] = a.x; v[r][1] = a.y; v[r][2] = a.z; v[r][3] = a.w;
+    v[r][4] = b.x; v[r][5] = b.y; v[r][6] = b.z; v[r][7] = b.w;
+  }
+  // block sum of a k x k block at (r0, c0), row-major sequential from 0 (torch's order)
+  auto bsum = [&](int r0, int c0, int k) {
+    float s = 0.f;
+    for (int r = 0; r < k; ++r)
+      for (int c = 0; c < k; ++c) s += v[r0 + r][c0 + c];
+    return s;
+  };
+  const int W1 = W >> 1, W2 = W >> 2, W3 = W >> 3;
+  float* p1 = o1 + pl * (H >> 1) * W1 + (by * 4) * W1 + bx * 4;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    float q[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) q[c] = bsum(2 * r, 2 * c, 2) / 2.f / 2.f;
+    reinterpret_cast<float4*>(p1 + r * W1)[0] = make_float4(q[0], q[1], q[2], q[3]);
+  }
+  float* p2 = o2 + pl * (H >> 2) * W2 + (by * 2) * W2 + bx * 2;
+#pragma unroll
+  for (int r = 0; r < 2; ++r)
+    reinterpret_cast<float2*>(p2 + r * W2)[0] =
+        make_float2(bsum(4 * r, 0, 4) / 4.f / 4.f, bsum(4 * r, 4, 4) / 4.f / 4.f);
+  o3[pl * (H >> 3) * W3 + by * W3 + bx] = bsum(0, 0, 8) / 8.f / 8.f;
+}
+
 inline float ac_scale(int in, int out) {
   return out > 1 ? (float)(in - 1) / (float)(out - 1) : 0.f;
 }
@@ -112,6 +165,14 @@ hipError_t upsample_bwd_launch(const float* gout, float* gx, int B, int C, int H
   const long long n = planes * H * W;
   hipLaunchKernelGGL(upsample_bwd_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, gout,
                      gx, planes, H, W, Ho, Wo, ac_scale(H, Ho), ac_scale(W, Wo), (float)k);
+  return hipGetLastError();
+}
+
+hipError_t area_pyramid_launch(const float* x, float* o1, float* o2, float* o3, long long planes,
+                               int H, int W, hipStream_t s) {
+  const long long n = planes * (H / 8) * (W / 8);
+  hipLaunchKernelGGL(area_pyramid_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, x, o1, o2,
+                     o3, planes, H, W);
   return hipGetLastError();
 }
 

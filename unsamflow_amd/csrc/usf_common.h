@@ -49,6 +49,11 @@ struct FwdEpi {
   long long out_bstride;
   int act;
   float slope;
+  // channel split (set by the dispatcher): groups > 1 -> every workgroup sums
+  // a channel group and writes raw partials to part[g][b][k][p]; a reduce
+  // kernel applies the mean and the epilogue. Not part of the C ABI.
+  float* part = nullptr;
+  int groups = 1;
 };
 struct BwdEpi {
   long long g_bstride;
@@ -57,7 +62,10 @@ hipError_t leaky_bwd_gather_launch(const float* g, const float* act, long long g
                                    float slope, float* out, int B, int K2, int H, int W,
                                    hipStream_t s);
 hipError_t corr_fwd_launch(const float* x1, const float* x2, float* out, int B, int C,
-                           int H, int W, int d, hipStream_t s, FwdEpi ep);
+                           int H, int W, int d, hipStream_t s, FwdEpi ep, float* workspace = nullptr,
+                           long long workspace_floats = 0);
+// floats of workspace that lets the forward split its channel loop (0: no split)
+long long corr_fwd_workspace(int B, int C, int H, int W, int d);
 hipError_t corr_bwd_launch(const float* x1, const float* x2, const float* gout,
                            float* gx1, float* gx2, int B, int C, int H, int W, int d,
                            hipStream_t s, BwdEpi ep);
@@ -88,5 +96,7 @@ hipError_t upsample_fwd_launch(const float* x, float* out, int B, int C, int H, 
                                hipStream_t s);
 hipError_t upsample_bwd_launch(const float* gout, float* gx, int B, int C, int H, int W, int k,
                                hipStream_t s);
+hipError_t area_pyramid_launch(const float* x, float* o1, float* o2, float* o3, long long planes,
+                               int H, int W, hipStream_t s);
 
 }  // namespace usf

@@ -140,9 +140,26 @@ class unFlowLoss(nn.Module):  # noqa: N801 (reference name)
             return fn(flow, im1_scaled, edge="image", alpha=self.cfg.edge_aware_alpha).mean()
         return fn(flow, im1_scaled, edge="full_seg", full_seg=kw["full_seg"]).mean()
 
+    def _image_pyramid(self, im, sizes):
+        """{(h, w): F.interpolate(im, (h, w), mode="area")} for the loss scales,
+        from one HIP pass (ops.area_pyramid, bit-exact) when the sizes are the
+        exact halvings it computes; None otherwise (torch per scale)."""
+        if not (self.fused and im.is_cuda):
+            return None
+        H, W = im.shape[-2:]
+        want = {(H >> s, W >> s) for s in range(4)}
+        if H % 8 or W % 8 or not set(sizes) <= want:
+            return None
+        from . import ops
+
+        return dict(zip([(H >> s, W >> s) for s in range(4)], [im] + ops.area_pyramid(im)))
+
     def loss_one_pair(self, pyramid_flows, im1_origin, im2_origin, occ_aware=True, **kw):
         c = self.cfg
         dev = pyramid_flows[0].device
+        sizes = [tuple(f.shape[-2:]) for i, f in enumerate(pyramid_flows) if c.w_ph_scales[i] > 0]
+        pyr1 = self._image_pyramid(im1_origin, sizes)
+        pyr2 = self._image_pyramid(im2_origin, sizes) if pyr1 is not None else None
         top = pyramid_flows[0]
         scale = min(*top.shape[-2:])
         if c.occ_from_back:
@@ -157,14 +174,17 @@ class unFlowLoss(nn.Module):  # noqa: N801 (reference name)
             vis1_pyr.append(F.interpolate(vis1, hw, mode="nearest"))
             vis2_pyr.append(F.interpolate(vis2, hw, mode="nearest"))
 
-        zero = torch.tensor(0, dtype=torch.float32, device=dev)
+        zero = torch.zeros((), dtype=torch.float32, device=dev)  # a fill, not an H2D copy (graph-capturable)
         warp_losses, smooth_losses = [], []
         for i, flow in enumerate(pyramid_flows):
             b, _, h, w = flow.size()
             im1_s = im2_s = None
             if c.w_ph_scales[i] > 0:
-                im1_s = F.interpolate(im1_origin, (h, w), mode="area")
-                im2_s = F.interpolate(im2_origin, (h, w), mode="area")
+                if pyr1 is not None:  # F.interpolate(im, (h, w), mode="area") from the HIP pyramid
+                    im1_s, im2_s = pyr1[(h, w)], pyr2[(h, w)]
+                else:
+                    im1_s = F.interpolate(im1_origin, (h, w), mode="area")
+                    im2_s = F.interpolate(im2_origin, (h, w), mode="area")
                 if occ_aware:
                     m1, m2 = vis1_pyr[i], vis2_pyr[i]
                 else:

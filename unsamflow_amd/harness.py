@@ -60,7 +60,8 @@ class TrainStep:
 
     def __init__(self, cfg, device, ddp: bool = False, corr_module=None, warp_fn: Callable | None = None,
                  loss_kwargs: dict | None = None, fused_adam: bool | None = None, seed: int = 42,
-                 channels_last: bool = False, occ_backward_fn: Callable | None = None):
+                 channels_last: bool = False, occ_backward_fn: Callable | None = None,
+                 capturable: bool = False):
         torch.manual_seed(seed)
         self.cfg = cfg
         self.device = torch.device(device)
@@ -77,8 +78,12 @@ class TrainStep:
         t = cfg.train
         if fused_adam is None:
             fused_adam = self.device.type == "cuda"
-        self.optimizer = torch.optim.Adam(param_groups(self.module, t), t.lr, betas=(t.momentum, t.beta), eps=1e-7,
-                                          fused=fused_adam or None)
+        # capturable: the step counters and the learning rate live on the device
+        # (the scheduler fills the lr tensor in place), so the step can be
+        # captured into a HIP graph (GraphedTrainStep)
+        lr = torch.tensor(float(t.lr), device=self.device) if capturable else t.lr
+        self.optimizer = torch.optim.Adam(param_groups(self.module, t), lr, betas=(t.momentum, t.beta), eps=1e-7,
+                                          fused=fused_adam or None, capturable=capturable)
         sched = t.get("lr_scheduler")
         if sched and sched.module == "OneCycleLR":
             p = dict(sched.params)
@@ -105,6 +110,119 @@ class TrainStep:
         self.optimizer.step()
         self.scheduler.step()
         return loss.detach()
+
+
+class FlatGrads:
+    """Every parameter's .grad as a view of one flat fp32 buffer: static
+    addresses for graph capture, and ONE all-reduce bucket per step for data
+    parallelism (10 MB for PWCLite: one RCCL ring all-reduce over xGMI instead
+    of DDP's per-bucket hooks). Backward accumulates into the views, so the
+    buffer is zeroed at the start of every step."""
+
+    def __init__(self, params):
+        self.params = [p for p in params if p.requires_grad]
+        n = sum(p.numel() for p in self.params)
+        dev = self.params[0].device
+        self.flat = torch.zeros(n, device=dev, dtype=torch.float32)
+        off = 0
+        for p in self.params:
+            p.grad = self.flat[off:off + p.numel()].view_as(p)
+            off += p.numel()
+
+    def zero_(self):
+        self.flat.zero_()
+
+    def all_reduce_mean(self, group=None):
+        import torch.distributed as dist
+
+        world = dist.get_world_size(group)
+        if world > 1:
+            dist.all_reduce(self.flat, group=group)
+            self.flat.div_(world)
+
+
+def broadcast_params(module: torch.nn.Module, src: int = 0, group=None) -> None:
+    """Replicas start from rank ``src``'s weights (what DDP's constructor does)."""
+    import torch.distributed as dist
+
+    with torch.no_grad():
+        for t in list(module.parameters()) + list(module.buffers()):
+            dist.broadcast(t, src, group=group)
+
+
+class GraphedTrainStep:
+    """The TrainStep replayed from HIP graphs (torch.cuda.CUDAGraph): the ~4k
+    kernel launches of a PWCLite step (MIOpen convolutions, torch elementwise
+    work and this library's kernels) are captured once and re-issued by one
+    graph launch, so the step no longer pays per-launch host cost.
+
+    Single process: one graph = zero grads + fwd(with_bk) + unFlowLoss + bwd +
+    clip_grad_norm_ + Adam(capturable). Data parallel (world > 1): graph A =
+    zero + fwd + loss + bwd into the flat gradient buffer, then one eager
+    all-reduce of that buffer over RCCL, then graph B = clip + Adam. OneCycleLR
+    runs eagerly between replays (it fills the device lr tensor in place).
+    Inputs are static buffers: ``load()`` copies new frames in before a replay.
+    """
+
+    def __init__(self, step: TrainStep, img1, img2, full_seg1=None, full_seg2=None, warmup: int = 3,
+                 group=None):
+        import torch.distributed as dist
+
+        self.step = step
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+        self.inputs = [None if t is None else t.clone() for t in (img1, img2, full_seg1, full_seg2)]
+        self.grads = FlatGrads(step.module.parameters())
+        dev = step.device
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):  # allocator pools, solver selection, optimizer state
+            for _ in range(warmup):
+                self._fwd_bwd()
+                self._reduce()
+                self._update()
+        torch.cuda.current_stream(dev).wait_stream(side)
+        torch.cuda.synchronize(dev)
+        if self.world == 1:
+            self.graph_a = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.graph_a):
+                self.loss = self._fwd_bwd()
+                self._update()
+            self.graph_b = None
+        else:
+            self.graph_a = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.graph_a):
+                self.loss = self._fwd_bwd()
+            self.graph_b = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.graph_b, pool=self.graph_a.pool()):
+                self._update()
+
+    def _fwd_bwd(self):
+        self.grads.zero_()
+        loss, _ = self.step.forward_loss(*self.inputs)
+        loss.backward()
+        return loss.detach()
+
+    def _reduce(self):
+        if self.world > 1:
+            self.grads.all_reduce_mean(self.group)
+
+    def _update(self):
+        torch.nn.utils.clip_grad_norm_(self.grads.params, self.step.max_grad_norm)
+        self.step.optimizer.step()
+
+    def load(self, img1, img2, full_seg1=None, full_seg2=None):
+        for dst, src in zip(self.inputs, (img1, img2, full_seg1, full_seg2)):
+            if dst is not None:
+                dst.copy_(src)
+
+    def __call__(self):
+        self.graph_a.replay()
+        if self.graph_b is not None:
+            self._reduce()
+            self.graph_b.replay()
+        self.step.scheduler.step()
+        return self.loss
 
 
 def smoke_step(device) -> None:

@@ -79,14 +79,16 @@ def warp_bytes(B, C, H, W, backward=False, need_x=True, need_flow=True):
 
 
 class KernelTimer:
-    def __init__(self, time_in_step: bool = True):
+    def __init__(self, time_in_step: bool = True, enabled: bool = True):
         self.time_in_step = time_in_step
+        self.enabled = enabled  # False: a no-op context (nothing recorded)
         self.records = []  # (op, key, start_event, end_event, bytes, flops)
 
     def __enter__(self):
         global _active
         self._prev = _active
-        _active = self
+        if self.enabled:
+            _active = self
         return self
 
     def __exit__(self, *exc):
@@ -161,6 +163,9 @@ def site_launcher(op: str, key, device, seed: int = 0):
             return lambda: ops.flow_upsample(f, k)
         go = torch.randn(B, C, H * k, W * k, device=device, generator=g)
         return lambda: ops.flow_upsample_backward(go, k)
+    if op == "area_pyramid":
+        img = torch.rand(*key, device=device, generator=g)
+        return lambda: ops.area_pyramid(img)
     if op == "photo_bwd":
         B, ndir, H, W = key
         basis = torch.randn(B, 4 * ndir, H, W, device=device, generator=g)

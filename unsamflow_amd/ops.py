@@ -62,14 +62,27 @@ def corr_forward(x1: torch.Tensor, x2: torch.Tensor, max_displacement: int,
     else:
         _check_out("output", out, (B, K * K, H, W), x1.device)
     lib = _lib.load()
+    ws, nws = _corr_workspace(lib, B, C, H, W, d, x1.device)
     with torch.cuda.device(x1.device), _kt.timed(
         "corr_fwd", (B, C, H, W), x1.device, _kt.corr_bytes(B, C, H, W, K * K), _kt.corr_flops(B, C, H, W, K * K)
     ):
-        rc = lib.usf_corr_fwd_f32(
-            x1c.data_ptr(), x2c.data_ptr(), out.data_ptr(), B, C, H, W, d, _lib.stream_handle(x1.device)
+        # the _ex entry with a dense output stride: same result as usf_corr_fwd_f32,
+        # plus the channel-split workspace for the small levels
+        rc = lib.usf_corr_fwd_ex_f32(
+            x1c.data_ptr(), x2c.data_ptr(), out.data_ptr(), K * K * H * W, 0, 0.0,
+            ws.data_ptr() if nws else None, nws, B, C, H, W, d, _lib.stream_handle(x1.device)
         )
-    _lib.check(rc, "usf_corr_fwd_f32")
+    _lib.check(rc, "usf_corr_fwd_ex_f32")
     return out
+
+
+def _corr_workspace(lib, B, C, H, W, d, device):
+    """Caller-provided scratch for the forward's channel split (torch's caching
+    allocator; empty when the shape does not split)."""
+    n = int(lib.usf_corr_fwd_workspace(B, C, H, W, d))
+    if n <= 0:
+        return None, 0
+    return torch.empty(n, device=device, dtype=torch.float32), n
 
 
 def corr_backward(
@@ -356,11 +369,13 @@ def corr_forward_ex(x1: torch.Tensor, x2: torch.Tensor, max_displacement: int, o
     x1c, x2c = x1.contiguous(), x2.contiguous()
     lib = _lib.load()
     act = 0 if leaky_slope is None else 1
+    ws, nws = _corr_workspace(lib, B, C, H, W, d, x1.device)
     with torch.cuda.device(x1.device), _kt.timed(
         "corr_fwd", (B, C, H, W), x1.device, _kt.corr_bytes(B, C, H, W, K * K), _kt.corr_flops(B, C, H, W, K * K)
     ):
         rc = lib.usf_corr_fwd_ex_f32(x1c.data_ptr(), x2c.data_ptr(), out.data_ptr(), obs, act,
-                                     float(leaky_slope or 0.0), B, C, H, W, d, _lib.stream_handle(x1.device))
+                                     float(leaky_slope or 0.0), ws.data_ptr() if nws else None, nws,
+                                     B, C, H, W, d, _lib.stream_handle(x1.device))
     _lib.check(rc, "usf_corr_fwd_ex_f32")
     return out
 
@@ -434,3 +449,22 @@ def flow_upsample_backward(grad_out: torch.Tensor, factor: int) -> torch.Tensor:
                                            _lib.stream_handle(grad_out.device))
     _lib.check(rc, "usf_flow_upsample_bwd_f32")
     return gx
+
+
+def area_pyramid(x: torch.Tensor):
+    """The loss's image pyramid: ``[F.interpolate(x, (H >> s, W >> s), mode="area")
+    for s in 1, 2, 3]`` (flow_loss.py:118-125), one read of x, bit-exact with
+    torch's CPU kernel. x: [B,C,H,W] fp32 on the device, H and W multiples of 8."""
+    _require_device_f32("x", x)
+    B, C, H, W = _nchw("x", x)
+    if H % 8 or W % 8:
+        raise ValueError(f"area_pyramid needs H, W multiples of 8, got {H}x{W}")
+    xc = x.contiguous()
+    outs = [torch.empty((B, C, H >> s, W >> s), device=x.device, dtype=torch.float32) for s in (1, 2, 3)]
+    lib = _lib.load()
+    nbytes = 4 * B * C * H * W * (1 + 1 / 4 + 1 / 16 + 1 / 64)
+    with torch.cuda.device(x.device), _kt.timed("area_pyramid", (B, C, H, W), x.device, int(nbytes)):
+        rc = lib.usf_area_pyramid_f32(xc.data_ptr(), outs[0].data_ptr(), outs[1].data_ptr(), outs[2].data_ptr(),
+                                      B, C, H, W, _lib.stream_handle(x.device))
+    _lib.check(rc, "usf_area_pyramid_f32")
+    return outs
