@@ -16,7 +16,10 @@ FLAGS = ["-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950"]
 def build(name, defines):
     OUT.mkdir(parents=True, exist_ok=True)
     objs = []
-    for src in ("corr.hip", "warp.hip", "capi.cpp"):
+    sys.path.insert(0, str(REPO))
+    from unsamflow_amd.build import SOURCES
+
+    for src in SOURCES:
         obj = OUT / f"{name}_{Path(src).stem}.o"
         lang = ["-x", "hip"] if src.endswith(".hip") else []
         subprocess.run(["/opt/rocm/bin/hipcc", *FLAGS, *defines, *lang, "-c", str(CSRC / src), "-o", str(obj)],

@@ -14,14 +14,21 @@ from unsamflow_amd.kernel_timer import site_launcher  # noqa: E402
 KITTI = [(192, 4, 13), (128, 8, 26), (96, 16, 52), (64, 32, 104), (32, 64, 208)]
 SITES = [("corr_fwd", (8, C, H, W)) for C, H, W in KITTI]
 SITES += [("corr_bwd", (8, C, H, W, True, True)) for C, H, W in KITTI]
+SITES += [("corr_bwd_leaky", (8, C, H, W, True, True)) for C, H, W in KITTI]
 SITES += [("warp_fwd", (8, C, H, W, "border")) for C, H, W in KITTI[1:]]
 SITES += [("warp_bwd", (8, C, H, W, "border", True, True)) for C, H, W in KITTI[1:]]
 SITES += [("warp_fwd", (8, 3, 256, 832, "border")), ("warp_bwd", (8, 3, 256, 832, "border", False, True))]
-SITES += [("occ_bwd", (8, 1, 256, 832))]
+SITES += [("occ_bwd", (8, 1, 256, 832)), ("area_pyramid", (8, 3, 256, 832))]
 SITES += [("photo_fwd", (8, 3, 256 >> i, 832 >> i, "border")) for i in range(4)]
 SITES += [("photo_fwd_grad", (8, 3, 256 >> i, 832 >> i, "border")) for i in range(4)]
 SITES += [("photo_pair_grad", (8, 3, 256 >> i, 832 >> i, "border")) for i in range(4)]
 SITES += [("photo_bwd", (8, 2, 256 >> i, 832 >> i)) for i in range(4)]
+
+
+def selected_sites():
+    """SITES, or the subset whose op is listed in KPROF_OPS (comma-separated)."""
+    only = os.environ.get("KPROF_OPS")
+    return [s for s in SITES if not only or s[0] in only.split(",")]
 
 
 def main():
@@ -33,9 +40,7 @@ def main():
     b = torch.empty_like(a)
     for _ in range(n):
         b.copy_(a)
-    only = os.environ.get("KPROF_OPS")  # e.g. "photo_fwd_grad,photo_bwd": a subset of the sites
-    sites = [s for s in SITES if not only or s[0] in only.split(",")]
-    for op, key in sites:
+    for op, key in selected_sites():
         fn = site_launcher(op, key, dev)
         for _ in range(n):
             fn()

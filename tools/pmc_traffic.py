@@ -42,7 +42,7 @@ def per_dispatch(path, counter):
 
 def main():
     root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc"
-    from kprof import SITES
+    from kprof import selected_sites
     from unsamflow_amd.kernel_timer import corr_bytes, warp_bytes
 
     n = int(os.environ.get("KPROF_N", "3"))
@@ -57,12 +57,17 @@ def main():
     uf = [v for name, v in fetch if "usf::" in name]
     uw = [v for name, v in write if "usf::" in name]
     # library kernels per launch of a site (summed): splat + threshold, partials + final
-    per_launch = {"occ_bwd": 2, "photo_fwd": 2, "photo_fwd_grad": 2, "photo_pair_grad": 2}
+    per_launch = {"occ_bwd": 2, "photo_fwd": 2, "photo_fwd_grad": 2, "photo_pair_grad": 2, "corr_bwd_leaky": 2}
     # kernels a site's launcher runs once before its timed launches
     prefix = {}
     sites, pos = [], 0
-    for op, key in SITES:
+    from unsamflow_amd import _lib
+
+    lib = _lib.load()  # host-only query: split forwards run a second (reduce) kernel
+    for op, key in selected_sites():
         k = per_launch.get(op, 1)
+        if op == "corr_fwd" and lib.usf_corr_fwd_workspace(*key[:4], 4) > 0:
+            k = 2
         pos += prefix.get(op, 0)
         fk = statistics.median(sum(uf[pos + j * k + i] for i in range(k)) for j in range(n))
         wk = statistics.median(sum(uw[pos + j * k + i] for i in range(k)) for j in range(n))
@@ -72,11 +77,15 @@ def main():
         else:
             B, C, H, W = key[:4]
         if op.startswith("corr"):
-            alg = corr_bytes(*key[:4], backward=op == "corr_bwd")
+            alg = corr_bytes(*key[:4], backward=op.startswith("corr_bwd"))
+            if op == "corr_bwd_leaky":
+                alg += 4 * B * H * W * 81  # the activated output read by the LeakyReLU derivative
         elif op == "warp_fwd":
             alg = warp_bytes(*key[:4])
         elif op == "warp_bwd":
             alg = warp_bytes(*key[:4], True, key[5], key[6])
+        elif op == "area_pyramid":
+            alg = int(4 * B * C * H * W * (1 + 1 / 4 + 1 / 16 + 1 / 64))
         elif op == "occ_bwd":
             alg = 4 * B * H * W * 3  # flow in, mask out (ops.occ_backward)
         elif op == "photo_fwd":

@@ -5,7 +5,10 @@ Reads the JSON line of a bench.py run made under
 and that run's kernel_stats.csv, where every hot-path launch is listed under
 its call-site name (unsamflow_amd.kernel_timer.site_name). Prints, for the
 roofline site and every other hot-path site, the bench's in-step event mean
-next to rocprof's average duration (rocprof also counts the warm-up steps).
+next to rocprof's summed kernel duration per launch of that site (rocprof
+also counts the warm-up steps; a site whose launch runs two kernels -- the
+split forward's reduce, the leaky backward's derivative pass, the photometric
+final reduction -- is the sum of both).
 
 Usage: python tools/roofline_check.py bench_prof.json run_kernel_stats.csv
 """
@@ -18,12 +21,16 @@ def main():
     bench = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
     stats = {r["Name"]: r for r in csv.DictReader(open(sys.argv[2]))}
     roof = bench["roofline"]
+    steps = bench["steps"] + bench["warmup"]
     sites = []
     for row in bench["levels"]:
         st = stats.get(row["site"])
-        entry = {"site": row["site"], "bench_in_step_us": row["in_step_us"],
-                 "rocprof_avg_us": round(float(st["AverageNs"]) / 1e3, 2) if st else None,
+        entry = {"site": row["site"], "bench_in_step_us": row["in_step_us"], "rocprof_avg_us": None,
                  "rocprof_calls": int(st["Calls"]) if st else None}
+        if st:
+            launches = row["calls_per_step"] * steps
+            entry["kernels_per_launch"] = max(1, round(int(st["Calls"]) / launches))
+            entry["rocprof_avg_us"] = round(float(st["TotalDurationNs"]) / 1e3 / launches, 2)
         if st:
             entry["rel_diff"] = round(entry["rocprof_avg_us"] / row["in_step_us"] - 1, 4)
         sites.append(entry)

@@ -25,7 +25,7 @@ def site_list(ops):
     for op in ops:
         if op == "corr_fwd":
             out += [(op, (8, C, H, W)) for C, H, W in KITTI]
-        elif op == "corr_bwd":
+        elif op in ("corr_bwd", "corr_bwd_leaky"):
             out += [(op, (8, C, H, W, True, True)) for C, H, W in KITTI]
         elif op == "warp_fwd":
             out += [(op, (8, C, H, W, "border")) for C, H, W in KITTI[1:]]
@@ -53,6 +53,8 @@ def alg_bytes(op, key):
         return 4 * B * H * W * (2 * C + 81)
     if op == "corr_bwd":
         return 4 * B * H * W * (81 + 4 * C)
+    if op == "corr_bwd_leaky":
+        return 4 * B * H * W * (2 * 81 + 4 * C)
     if op == "warp_fwd":
         return 4 * B * H * W * (2 * C + 2)
     if op == "warp_bwd":

@@ -718,8 +718,11 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(USF_BWD
   USF_TRACE_HWID();
   // work item: channel group fastest (the groups of a tile share its g planes),
   // then tile, then (direction, sample); grid = (tiles, groups, B * dirs).
-  // No XCD remap here: tools/ab_build.py A/B on the box, L4 59 us without vs
-  // 85 us with it (FETCH traffic 2.6x -> 1.4x of algorithmic, yet slower).
+  // No XCD remap here. Measured twice on the box (tools/ab_build.py): remapping
+  // this order (L4 85 vs 59 us) and a direction-fastest order dealt to the XCDs
+  // in contiguous chunks, so a tile's gx1/gx2 and its neighbours share one L2
+  // (L4 84 vs 59 us, L3 51 vs 43 us) are both slower, although they cut the
+  // FETCH traffic (2.6x -> 1.4x of algorithmic).
   const int w = linear_block();
   const int group = w % gridDim.y;
   const int tile = (w / gridDim.y) % gridDim.x;

@@ -147,6 +147,13 @@ def site_launcher(op: str, key, device, seed: int = 0):
     from . import ops
 
     g = torch.Generator(device=device).manual_seed(seed)
+    if op == "corr_bwd_leaky":  # the decoder's site: g from a concat slice + LeakyReLU derivative
+        B, C, H, W = key[:4]
+        x1 = torch.randn(B, C, H, W, device=device, generator=g)
+        x2 = torch.randn(B, C, H, W, device=device, generator=g)
+        cat = torch.randn(B, 81 + C + 2, H, W, device=device, generator=g)
+        act = torch.nn.functional.leaky_relu(torch.randn(B, 81 + C + 2, H, W, device=device, generator=g), 0.1)
+        return lambda: ops.corr_backward_ex(x1, x2, cat[:, :81], 4, key[4], key[5], act_out=act[:, :81])
     if op in ("corr_fwd", "corr_bwd"):
         B, C, H, W = key[:4]
         x1 = torch.randn(B, C, H, W, device=device, generator=g)

@@ -405,9 +405,14 @@ def corr_backward_ex(x1: torch.Tensor, x2: torch.Tensor, grad_out: torch.Tensor,
     g1 = torch.empty_like(x1c) if need_x1 else None
     g2 = torch.empty_like(x2c) if need_x2 else None
     lib = _lib.load()
+    # with the LeakyReLU derivative the site also reads the activated output
+    # once (what leaky_relu_backward needs): a distinct site, its bytes included
+    op = "corr_bwd" if act_out is None else "corr_bwd_leaky"
+    nbytes = _kt.corr_bytes(B, C, H, W, K * K, True, need_x1, need_x2)
+    if act_out is not None:
+        nbytes += 4 * B * H * W * K * K
     with torch.cuda.device(x1.device), _kt.timed(
-        "corr_bwd", (B, C, H, W, need_x1, need_x2), x1.device,
-        _kt.corr_bytes(B, C, H, W, K * K, True, need_x1, need_x2),
+        op, (B, C, H, W, need_x1, need_x2), x1.device, nbytes,
         _kt.corr_flops(B, C, H, W, K * K, True, need_x1, need_x2),
     ):
         rc = lib.usf_corr_bwd_ex_f32(x1c.data_ptr(), x2c.data_ptr(), grad_out.data_ptr(), gbs, _ptr(act_out),
