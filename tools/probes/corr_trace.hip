@@ -65,9 +65,9 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&tr, max_waves * usf::kTraceSlots * 8));
   auto run = [&]() {
     if (fwd)
-      CK(usf::corr_fwd_launch(x1, x2, o, B, C, H, W, 4, nullptr));
+      CK(usf::corr_fwd_launch(x1, x2, o, B, C, H, W, 4, nullptr, usf::FwdEpi{81LL * H * W, 0, 0.f}));
     else
-      CK(usf::corr_bwd_launch(x1, x2, g, o, o2, B, C, H, W, 4, nullptr));  // both directions
+      CK(usf::corr_bwd_launch(x1, x2, g, o, o2, B, C, H, W, 4, nullptr, usf::BwdEpi{81LL * H * W}));  // both directions
   };
   for (int i = 0; i < 5; ++i) run();  // warm, untraced
   CK(hipDeviceSynchronize());
