@@ -39,6 +39,8 @@ def site_list(ops):
             out += [(op, (8, 1, 256, 832))]
         elif op == "area_pyramid":
             out += [(op, (8, 3, 256, 832))]
+        elif op in ("upsample", "upsample_bwd"):
+            out += [(op, (8, 2, H, W, 2)) for _, H, W in KITTI[:4]]
         else:
             raise SystemExit(f"unknown op {op}")
     return out
@@ -69,6 +71,10 @@ def alg_bytes(op, key):
         return 2 * 4 * B * H * W * (2 * C + 7)
     if op == "occ_bwd":
         return 4 * B * H * W * 3
+    if op == "upsample":
+        return 4 * B * C * H * W * 5  # read x, write the 4x larger output
+    if op == "upsample_bwd":
+        return 4 * B * C * H * W * 5
     if op == "area_pyramid":
         return int(4 * B * C * H * W * (1 + 1 / 4 + 1 / 16 + 1 / 64))
     raise KeyError(op)

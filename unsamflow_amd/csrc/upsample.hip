@@ -17,6 +17,9 @@
 // row-major order, then / k / k (torch's CPU order, bit-exact; the divisions
 // are by powers of two). One thread reads an 8x8 block once (16 float4 loads)
 // and writes all three coarser scales.
+#include <algorithm>
+#include <cmath>
+
 #include "usf_common.h"
 
 namespace usf {
@@ -64,6 +67,18 @@ __device__ __forceinline__ float axis_weight(const Lin& t, int in_i) {
   return w;
 }
 
+// output rows whose taps can touch input row i: src in (i - 1, i + 1] (a
+// generous window, filtered exactly by axis_weight)
+__device__ __forceinline__ void tap_window(int i, float s, int out, int& o0, int& o1) {
+  o0 = s > 0.f ? max(0, (int)floorf((i - 1) / s) - 1) : 0;
+  o1 = s > 0.f ? min(out - 1, (int)ceilf((i + 1) / s) + 1) : out - 1;
+}
+
+// NWIN > 0: every window fits NWIN rows / columns (checked on the host), so
+// the weights are computed once per axis and all loads are issued
+// unconditionally at clamped offsets (zero weights outside the window: adding
+// 0 * g leaves the sums unchanged). NWIN == 0: the generic loop.
+template <int NWIN>
 __global__ __launch_bounds__(256) void upsample_bwd_kernel(const float* __restrict__ gout,
                                                            float* __restrict__ gx, long long planes,
                                                            int H, int W, int Ho, int Wo, float sy,
@@ -76,22 +91,40 @@ __global__ __launch_bounds__(256) void upsample_bwd_kernel(const float* __restri
   const int iy = (int)((i / W) % H);
   const long long pl = i / ((long long)H * W);
   const float* gp = gout + pl * Ho * Wo;
-  // output rows whose taps can touch input row iy: src in (iy - 1, iy + 1]
-  // (a generous window, filtered exactly by axis_weight)
-  const int oy0 = sy > 0.f ? max(0, (int)floorf((iy - 1) / sy) - 1) : 0;
-  const int oy1 = sy > 0.f ? min(Ho - 1, (int)ceilf((iy + 1) / sy) + 1) : Ho - 1;
-  const int ox0 = sx > 0.f ? max(0, (int)floorf((ix - 1) / sx) - 1) : 0;
-  const int ox1 = sx > 0.f ? min(Wo - 1, (int)ceilf((ix + 1) / sx) + 1) : Wo - 1;
+  int oy0, oy1, ox0, ox1;
+  tap_window(iy, sy, Ho, oy0, oy1);
+  tap_window(ix, sx, Wo, ox0, ox1);
   float acc = 0.f;
-  for (int oy = oy0; oy <= oy1; ++oy) {
-    const float wy = axis_weight(lin_tap(oy, sy, H), iy);
-    if (wy == 0.f) continue;
-    float row = 0.f;
-    for (int ox = ox0; ox <= ox1; ++ox) {
-      const float wx = axis_weight(lin_tap(ox, sx, W), ix);
-      if (wx != 0.f) row += wx * gp[oy * Wo + ox];
+  if constexpr (NWIN > 0) {
+    float wx[NWIN];
+    int cx[NWIN];
+#pragma unroll
+    for (int j = 0; j < NWIN; ++j) {
+      const int ox = ox0 + j;
+      wx[j] = ox <= ox1 ? axis_weight(lin_tap(ox, sx, W), ix) : 0.f;
+      cx[j] = min(ox, Wo - 1);
     }
-    acc += wy * row;
+#pragma unroll
+    for (int r = 0; r < NWIN; ++r) {
+      const int oy = oy0 + r;
+      const float wy = oy <= oy1 ? axis_weight(lin_tap(oy, sy, H), iy) : 0.f;
+      const float* row_p = gp + min(oy, Ho - 1) * Wo;
+      float row = 0.f;
+#pragma unroll
+      for (int j = 0; j < NWIN; ++j) row += wx[j] * row_p[cx[j]];
+      acc += wy * row;
+    }
+  } else {
+    for (int oy = oy0; oy <= oy1; ++oy) {
+      const float wy = axis_weight(lin_tap(oy, sy, H), iy);
+      if (wy == 0.f) continue;
+      float row = 0.f;
+      for (int ox = ox0; ox <= ox1; ++ox) {
+        const float wx = axis_weight(lin_tap(ox, sx, W), ix);
+        if (wx != 0.f) row += wx * gp[oy * Wo + ox];
+      }
+      acc += wy * row;
+    }
   }
   gx[i] = acc * k;
 }
@@ -158,13 +191,33 @@ hipError_t upsample_fwd_launch(const float* x, float* out, int B, int C, int H, 
   return hipGetLastError();
 }
 
+// widest tap window over all input indices of one axis (host mirror of tap_window)
+static int max_window(int in, int out) {
+  const float s = ac_scale(in, out);
+  if (!(s > 0.f)) return out;
+  int m = 0;
+  for (int i = 0; i < in; ++i) {
+    const int o0 = std::max(0, (int)std::floor((i - 1) / s) - 1);
+    const int o1 = std::min(out - 1, (int)std::ceil((i + 1) / s) + 1);
+    m = std::max(m, o1 - o0 + 1);
+  }
+  return m;
+}
+
 hipError_t upsample_bwd_launch(const float* gout, float* gx, int B, int C, int H, int W, int k,
                                hipStream_t s) {
   const int Ho = H * k, Wo = W * k;
   const long long planes = (long long)B * C;
   const long long n = planes * H * W;
-  hipLaunchKernelGGL(upsample_bwd_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, gout,
-                     gx, planes, H, W, Ho, Wo, ac_scale(H, Ho), ac_scale(W, Wo), (float)k);
+  const dim3 grid((unsigned)((n + 255) / 256));
+  const float sy = ac_scale(H, Ho), sx = ac_scale(W, Wo);
+  const int win = std::max(max_window(H, Ho), max_window(W, Wo));
+  if (win <= 8)
+    hipLaunchKernelGGL(upsample_bwd_kernel<8>, grid, dim3(256), 0, s, gout, gx, planes, H, W, Ho, Wo, sy,
+                       sx, (float)k);
+  else
+    hipLaunchKernelGGL(upsample_bwd_kernel<0>, grid, dim3(256), 0, s, gout, gx, planes, H, W, Ho, Wo, sy,
+                       sx, (float)k);
   return hipGetLastError();
 }
 
