@@ -27,7 +27,7 @@
  *   usf_photo_loss_*  <- the per-scale warp + loss_photomatric composition of
  *                        losses/flow_loss.py:127-148
  *   usf_area_pyramid  <- the loss's per-scale F.interpolate(im, mode="area")
- *                        (losses/flow_loss.py:118-125)
+ *                        (losses/flow_loss.py:128-129)
  *   usf_flow_upsample_* <- F.interpolate(flow * k, scale_factor=k, bilinear,
  *                        align_corners=True) of the decoder (pwclite.py:299-301;
  *                        SURVEY §8f row 4)
@@ -173,7 +173,7 @@ int usf_photo_loss_fwd_f32(const float* src, const float* tgt, const float* mask
                            int pad_mode, float w_l1, float w_ssim, void* stream);
 
 /* Both directions of a with_bk scale in one launch (flow_loss.py:130-131,
- * 176-178 of the unFlowLoss): direction 0 warps im2 by flow[:, 0:2] onto im1
+ * 143-148): direction 0 warps im2 by flow[:, 0:2] onto im1
  * under mask1, direction 1 warps im1 by flow[:, 2:4] onto im2 under mask2.
  * flow: [B,4,H,W] with batch stride flow_bstride (dense [4,H,W] per sample);
  * partials: 2 * usf_photo_loss_partials(B,H,W) floats; out: 6 floats
@@ -206,7 +206,7 @@ int usf_flow_upsample_bwd_f32(const float* grad_out, float* grad_flow, int B, in
                               int W, int factor, void* stream);
 
 /* The loss's image pyramid (unFlowLoss per scale s: F.interpolate(im,
- * (H >> s, W >> s), mode="area"), flow_loss.py:118-125): out_s = mean of each
+ * (H >> s, W >> s), mode="area"), flow_loss.py:128-129): out_s = mean of each
  * 2^s x 2^s block, summed in row-major order as torch's CPU kernel does
  * (bit-exact). x: [B,C,H,W] dense with H % 8 == 0 and W % 8 == 0; out1/2/3:
  * [B,C,H/2,W/2], [B,C,H/4,W/4], [B,C,H/8,W/8] dense, overwritten. */

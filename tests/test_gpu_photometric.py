@@ -101,7 +101,7 @@ PAIR_CASES = [
 def test_photometric_pair_matches_reference_and_single_directions(hip_device, B, C, H, W, scale, pad):
     """Both with_bk directions in one launch == the two single-direction calls
     (bit-identical: same kernel body per direction) and == the reference
-    composition of each direction (flow_loss.py:130-131, 176-178)."""
+    composition of each direction (flow_loss.py:130-131, 143-148)."""
     from unsamflow_amd.photometric import photometric_loss, photometric_loss_pair
 
     seed = 300 + H + W

@@ -11,7 +11,7 @@
 // sums the weights of the few output rows / columns whose taps reach it
 // (ATen scatters with atomics), times k.
 //
-// Also the loss's image pyramid (flow_loss.py:118-125 of the reference's
+// Also the loss's image pyramid (flow_loss.py:128-129 of the reference's
 // unFlowLoss: F.interpolate(im, (H >> s, W >> s), mode="area") per scale s):
 // adaptive_avg_pool2d with exact 2^s blocks = the block's elements summed in
 // row-major order, then / k / k (torch's CPU order, bit-exact; the divisions

@@ -458,7 +458,7 @@ def flow_upsample_backward(grad_out: torch.Tensor, factor: int) -> torch.Tensor:
 
 def area_pyramid(x: torch.Tensor):
     """The loss's image pyramid: ``[F.interpolate(x, (H >> s, W >> s), mode="area")
-    for s in 1, 2, 3]`` (flow_loss.py:118-125), one read of x, bit-exact with
+    for s in 1, 2, 3]`` (flow_loss.py:128-129), one read of x, bit-exact with
     torch's CPU kernel. x: [B,C,H,W] fp32 on the device, H and W multiples of 8."""
     _require_device_f32("x", x)
     B, C, H, W = _nchw("x", x)
