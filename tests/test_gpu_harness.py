@@ -65,3 +65,27 @@ def test_train_step_full_kitti_size(hip_device):
     torch.cuda.synchronize()
     assert torch.isfinite(loss)
     assert not torch.equal(w0, step.module.conv_1x1[4][0].weight)
+
+
+def test_graphed_step_matches_eager_steps(hip_device):
+    """harness.GraphedTrainStep (the step captured into a HIP graph and replayed)
+    trains like TrainStep: same losses and parameters after the same number of
+    steps from the same state (up to the warp backward's atomic summation order)."""
+    from oracle.hashrng import uniform
+    from unsamflow_amd.config import kitti_base
+    from unsamflow_amd.harness import GraphedTrainStep, TrainStep
+
+    im1 = torch.from_numpy(uniform((2, 3, 64, 128), 31)).to(hip_device)
+    im2 = torch.from_numpy(uniform((2, 3, 64, 128), 32)).to(hip_device)
+    eager = TrainStep(kitti_base(), hip_device, capturable=True)
+    graphed = TrainStep(kitti_base(), hip_device, capturable=True)
+    losses_e = [float(eager(im1, im2)) for _ in range(3)]
+    g = GraphedTrainStep(graphed, im1, im2, warmup=1)  # 1 eager warm-up step, then capture
+    losses_g = [float(g()) for _ in range(2)]
+    torch.cuda.synchronize()
+    # the graph's first replay is step 2 (the warm-up was step 1)
+    np.testing.assert_allclose(losses_g, losses_e[1:], rtol=1e-4)
+    for (n, pe), pg in zip(eager.module.named_parameters(), graphed.module.parameters()):
+        torch.testing.assert_close(pg, pe, atol=1e-5, rtol=1e-4, msg=n)
+    assert float(graphed.optimizer.param_groups[0]["lr"]) == pytest.approx(
+        float(eager.optimizer.param_groups[0]["lr"]))

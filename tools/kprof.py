@@ -14,6 +14,8 @@ from unsamflow_amd.kernel_timer import site_launcher  # noqa: E402
 KITTI = [(192, 4, 13), (128, 8, 26), (96, 16, 52), (64, 32, 104), (32, 64, 208)]
 SITES = [("corr_fwd", (8, C, H, W)) for C, H, W in KITTI]
 SITES += [("corr_bwd", (8, C, H, W, True, True)) for C, H, W in KITTI]
+# one direction at a time (where the backward's traffic comes from)
+SITES += [("corr_bwd", (8, C, H, W, n1, not n1)) for C, H, W in KITTI[3:] for n1 in (True, False)]
 SITES += [("corr_bwd_leaky", (8, C, H, W, True, True)) for C, H, W in KITTI]
 SITES += [("warp_fwd", (8, C, H, W, "border")) for C, H, W in KITTI[1:]]
 SITES += [("warp_bwd", (8, C, H, W, "border", True, True)) for C, H, W in KITTI[1:]]

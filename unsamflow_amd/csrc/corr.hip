@@ -592,7 +592,14 @@ __device__ __forceinline__ void corr_bwd_tile(float* sm, const float* __restrict
   // or the dense [B,K*K,H,W] tensor
   const float* gb = g + (size_t)b * ep.g_bstride;
 
-  // this wave's DYW rows of g for its PX pixels, read once (clamped unconditional loads)
+  // this wave's DYW rows of g for its PX pixels, read once. All loads are
+  // unconditional at clamped in-bounds offsets (no branch, so no wait, inside
+  // the burst). With W % 4 == 0 (V == 4) each 4-pixel run is ONE 16-byte load:
+  // the dword form made every wave-instruction touch 8 cache lines for 32 of
+  // their 128 bytes, 4 times over (PMC: the backward is bound by its L2 request
+  // volume). gx2's runs start at xb - dx + d (dword aligned): the
+  // load is clamped into the row and the lanes at the image edge pick their
+  // elements out of it by index.
   float gv[DYW][K][PX];
 #pragma unroll
   for (int t = 0; t < DYW; ++t) {
@@ -601,12 +608,38 @@ __device__ __forceinline__ void corr_bwd_tile(float* sm, const float* __restrict
     for (int dx = 0; dx < K; ++dx) {
       const int k = min(dy, K - 1) * K + dx;
       const int yy = G2 ? y - dy + D : y;
+      if constexpr (USF_BWD_VECG && V == 4 && PX % 4 == 0) {
+        const bool rowok = dy < K && (unsigned)yy < (unsigned)H;
+        const float* row = gb + k * HW + (rowok ? yy : 0) * W;
 #pragma unroll
-      for (int i = 0; i < PX; ++i) {
-        const int xx = G2 ? xb + i - dx + D : xb + i;
-        const bool ok = dy < K && (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W;
-        const float v = gb[k * HW + (ok ? yy * W + xx : 0)];
-        gv[t][dx][i] = ok ? v : 0.f;
+        for (int i4 = 0; i4 < PX; i4 += 4) {
+          const int xs = G2 ? xb + i4 - dx + D : xb + i4;
+          const int xc = min(max(xs, 0), W - 4);
+          float4 v;
+          __builtin_memcpy(&v, row + xc, sizeof(v));
+          const int shift = xs - xc;  // 0 inside the image
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int xx = xs + i;
+            const bool ok = rowok && (unsigned)xx < (unsigned)W;
+            float e;
+            if constexpr (G2) {
+              const int idx = i + shift;
+              e = idx <= 0 ? v.x : idx == 1 ? v.y : idx == 2 ? v.z : v.w;
+            } else {
+              e = i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w;  // gx1 runs are aligned, never shifted
+            }
+            gv[t][dx][i4 + i] = ok ? e : 0.f;
+          }
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < PX; ++i) {
+          const int xx = G2 ? xb + i - dx + D : xb + i;
+          const bool ok = dy < K && (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W;
+          const float v = gb[k * HW + (ok ? yy * W + xx : 0)];
+          gv[t][dx][i] = ok ? v : 0.f;
+        }
       }
     }
   }
@@ -702,6 +735,9 @@ __device__ __forceinline__ void corr_bwd_tile(float* sm, const float* __restrict
 // 40 KB LDS, i.e. 3 waves/SIMD = 4 resident workgroups of 3 waves per CU.
 // amdgpu_waves_per_eu(3) pins the VGPR target: without it, allocation for the
 // two inlined direction bodies flips between 163 and 231 on unrelated edits.
+#ifndef USF_BWD_VECG
+#define USF_BWD_VECG 1
+#endif
 #ifndef USF_BWD_WAVES_PER_EU
 #define USF_BWD_WAVES_PER_EU 3
 #endif
@@ -723,7 +759,25 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(USF_BWD
   // in contiguous chunks, so a tile's gx1/gx2 and its neighbours share one L2
   // (L4 84 vs 59 us, L3 51 vs 43 us) are both slower, although they cut the
   // FETCH traffic (2.6x -> 1.4x of algorithmic).
-  const int w = linear_block();
+#ifndef USF_BWD_CHUNK
+#define USF_BWD_CHUNK 14
+#endif
+  int w = linear_block();
+  if (USF_BWD_CHUNK > 0 && gridDim.x >= 16) {
+    // Q consecutive work items per XCD, chunks dealt round-robin over the 8
+    // XCDs (block lin runs on XCD lin % 8; it gets item Q (8 m + x) + j): a few
+    // neighbouring tiles share their halo lines in one L2 while every XCD still
+    // gets a mix of samples and directions. L4 59.5 -> 54.5 us, L3 43 -> 40 us
+    // (profiles/ab_r01/bwd_chunk_*.json); whole-sample chunks (xcd_remap) are
+    // slower (84 us) and so are levels with < 16 tiles (L1 11.6 -> 13.5 us).
+    constexpr int Q = USF_BWD_CHUNK > 0 ? USF_BWD_CHUNK : 1;
+    const int n = gridDim.x * gridDim.y * gridDim.z;
+    const int full = (n / (8 * Q)) * (8 * Q);
+    if (w < full) {
+      const int x = w & 7, r = w >> 3;
+      w = Q * (8 * (r / Q) + x) + r % Q;
+    }
+  }
   const int group = w % gridDim.y;
   const int tile = (w / gridDim.y) % gridDim.x;
   int b = w / (gridDim.x * gridDim.y);

@@ -177,10 +177,11 @@ class GraphedTrainStep:
         side = torch.cuda.Stream(dev)
         side.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(side):  # allocator pools, solver selection, optimizer state
-            for _ in range(warmup):
+            for _ in range(warmup):  # real training steps, as TrainStep.__call__
                 self._fwd_bwd()
                 self._reduce()
                 self._update()
+                self.step.scheduler.step()
         torch.cuda.current_stream(dev).wait_stream(side)
         torch.cuda.synchronize(dev)
         if self.world == 1:
