@@ -538,6 +538,10 @@ hipError_t fwd_dispatch(const float* x1, const float* x2, float* out, int B, int
 }
 
 // --------------------------------------------------------------- backward --
+// 16-byte g loads in the backward prologue (tools/ab_build.py -DUSF_BWD_VECG=0: dword loads)
+#ifndef USF_BWD_VECG
+#define USF_BWD_VECG 1
+#endif
 template <int D, int PX, int SEGX, int NW, int CC, int V>
 struct BwdCfg {
   static constexpr int K = 2 * D + 1;
@@ -735,9 +739,6 @@ __device__ __forceinline__ void corr_bwd_tile(float* sm, const float* __restrict
 // 40 KB LDS, i.e. 3 waves/SIMD = 4 resident workgroups of 3 waves per CU.
 // amdgpu_waves_per_eu(3) pins the VGPR target: without it, allocation for the
 // two inlined direction bodies flips between 163 and 231 on unrelated edits.
-#ifndef USF_BWD_VECG
-#define USF_BWD_VECG 1
-#endif
 #ifndef USF_BWD_WAVES_PER_EU
 #define USF_BWD_WAVES_PER_EU 3
 #endif
