@@ -771,13 +771,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(USF_BWD
     // gets a mix of samples and directions. L4 59.5 -> 54.5 us, L3 43 -> 40 us
     // (profiles/ab_r01/bwd_chunk_*.json); whole-sample chunks (xcd_remap) are
     // slower (84 us) and so are levels with < 16 tiles (L1 11.6 -> 13.5 us).
-    constexpr int Q = USF_BWD_CHUNK > 0 ? USF_BWD_CHUNK : 1;
-    const int n = gridDim.x * gridDim.y * gridDim.z;
-    const int full = (n / (8 * Q)) * (8 * Q);
-    if (w < full) {
-      const int x = w & 7, r = w >> 3;
-      w = Q * (8 * (r / Q) + x) + r % Q;
-    }
+    w = xcd_chunk(w, gridDim.x * gridDim.y * gridDim.z, USF_BWD_CHUNK);
   }
   const int group = w % gridDim.y;
   const int tile = (w / gridDim.y) % gridDim.x;
