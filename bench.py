@@ -45,6 +45,7 @@ if REPO not in sys.path:
     sys.path.insert(0, REPO)
 
 import glob  # noqa: E402
+import re  # noqa: E402
 
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
@@ -147,7 +148,10 @@ def copy_ceiling_gbps(device, mib=512, reps=10):
 
 def pmc_traffic(op, shape):
     """HBM bytes per launch of (op, shape) from the newest committed PMC summary."""
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_traffic.json")))
+    def natural(path):  # r01_v12 after r01_v9
+        return [int(t) if t.isdigit() else t for t in re.split(r"(\d+)", os.path.basename(path))]
+
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_traffic.json")), key=natural)
     if not files:
         return None, None
     with open(files[-1]) as f:
