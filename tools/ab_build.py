@@ -10,7 +10,8 @@ from pathlib import Path
 REPO = Path(__file__).resolve().parent.parent
 CSRC = REPO / "unsamflow_amd" / "csrc"
 OUT = REPO / "unsamflow_amd" / "lib" / "ab"
-FLAGS = ["-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950"]
+sys.path.insert(0, str(REPO))
+from unsamflow_amd.build import COMMON_FLAGS as FLAGS  # noqa: E402  (the library's flags; A/B defines on top)
 
 
 def build(name, defines):

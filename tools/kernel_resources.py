@@ -18,8 +18,12 @@ REPO = Path(__file__).resolve().parent.parent
 def resources(src):
     with tempfile.TemporaryDirectory() as d:
         asm = Path(d) / "k.s"
-        subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950", "--cuda-device-only",
-                        "-S", "-o", str(asm), str(src)], check=True, capture_output=True)
+        sys.path.insert(0, str(REPO))
+        from unsamflow_amd.build import COMMON_FLAGS  # the library's own flags
+
+        flags = [f for f in COMMON_FLAGS if f != "-fPIC"]
+        subprocess.run(["/opt/rocm/bin/hipcc", *flags, "--cuda-device-only", "-S", "-o", str(asm), str(src)],
+                       check=True, capture_output=True)
         text = asm.read_text()
     out = []
     for name, body in re.findall(r"\.amdhsa_kernel (\S+)(.*?)\.end_amdhsa_kernel", text, re.S):
