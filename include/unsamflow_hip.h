@@ -116,10 +116,13 @@ long long usf_corr_fwd_workspace(int B, int C, int H, int W, int d);
  * same layout as gout) the LeakyReLU derivative g * (act_out > 0 ? 1 : slope)
  * is applied first -- torch's leaky_relu_backward on the result, as for the
  * in-place module -- in one dense pass into `scratch` (caller-provided,
- * B*(2d+1)^2*H*W floats; unused when act_out is NULL). */
+ * usf_corr_bwd_ex_scratch(B,C,H,W,d) floats; unused when act_out is NULL). */
 int usf_corr_bwd_ex_f32(const float* x1, const float* x2, const float* gout, long long g_bstride,
                         const float* act_out, float slope, float* scratch, float* gx1, float* gx2,
                         int B, int C, int H, int W, int d, void* stream);
+
+/* Floats of `scratch` usf_corr_bwd_ex_f32 needs with act_out at this shape (0: none). */
+long long usf_corr_bwd_ex_scratch(int B, int C, int H, int W, int d);
 
 /* Bilinear backward warp (flow_warp), align_corners=True.
  * x: [B,C,H,W]; flow: [B,2,H,W] with batch stride flow_bstride (elements);

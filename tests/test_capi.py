@@ -32,6 +32,7 @@ def test_header_declares_the_abi():
     assert syms == sorted(
         ["usf_abi_version", "usf_last_error_string", "usf_corr_fwd_f32", "usf_corr_bwd_f32",
          "usf_corr_fwd_ex_f32", "usf_corr_fwd_workspace", "usf_corr_bwd_ex_f32",
+         "usf_corr_bwd_ex_scratch",
          "usf_warp_fwd_f32", "usf_warp_bwd_f32", "usf_splat_map_f32", "usf_occ_backward_f32",
          "usf_photo_loss_partials", "usf_photo_loss_fwd_f32", "usf_photo_loss_pair_fwd_f32",
          "usf_photo_loss_bwd_f32",
@@ -82,7 +83,7 @@ def test_no_torch_types_in_abi():
         (lambda L: L.usf_corr_fwd_ex_f32(1, 1, 1, 10, 1, 0.1, None, 0, 2, 4, 4, 4, 4, None), "out batch stride"),
         (lambda L: L.usf_corr_fwd_ex_f32(1, 1, 1, 81 * 16, 7, 0.1, None, 0, 2, 4, 4, 4, 4, None), "unknown act"),
         (lambda L: L.usf_corr_bwd_ex_f32(1, 1, 1, 10, None, 0.1, None, 1, 1, 2, 4, 4, 4, 4, None), "gradient batch stride"),
-        (lambda L: L.usf_corr_bwd_ex_f32(1, 1, 1, 81 * 16, 1, 0.1, None, 1, 1, 2, 4, 4, 4, 4, None), "scratch"),
+        (lambda L: L.usf_corr_bwd_ex_f32(1, 1, 1, 81 * 20, 1, 0.1, None, 1, 1, 2, 4, 4, 5, 4, None), "scratch"),
         (lambda L: L.usf_flow_upsample_f32(1, 1, 1, 2, 4, 4, 0, None), "bad factor"),
         (lambda L: L.usf_flow_upsample_bwd_f32(None, 1, 1, 2, 4, 4, 2, None), "null pointer"),
         (lambda L: L.usf_splat_map_f32(1, 2 * 16, 1, 0, 4, 4, 0, None), "non-positive"),

@@ -40,6 +40,7 @@ _SIGNATURES = {
         ctypes.c_int,
     ),
     "usf_corr_fwd_workspace": ([ctypes.c_int] * 5, ctypes.c_longlong),
+    "usf_corr_bwd_ex_scratch": ([ctypes.c_int] * 5, ctypes.c_longlong),
     "usf_corr_bwd_ex_f32": (
         [_c_float_p] * 3 + [ctypes.c_longlong, _c_float_p, ctypes.c_float] + [_c_float_p] * 3
         + [ctypes.c_int] * 5 + [ctypes.c_void_p],

@@ -125,6 +125,24 @@ __device__ __forceinline__ void dma(const rsrc_t& rsrc, float* dst, int voff) {
 
 __device__ __forceinline__ void dma_wait_all() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
+// Buffer resource over `bytes` bytes at `p` (raw, stride 0) and a 16-byte load
+// through it at a byte offset: the address is one 32-bit VGPR.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t plane_buf(const float* p, int bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), 0, bytes, kRsrcFlags);
+}
+__device__ __forceinline__ float buf_load1(__amdgpu_buffer_rsrc_t r, int byte_off) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, byte_off, 0, 0));
+}
+using u32x4 = unsigned int __attribute__((ext_vector_type(4)));
+using f32x4 = float __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 buf_load4(__amdgpu_buffer_rsrc_t r, int byte_off) {
+  // explicitly typed: with `auto` and per-element bit casts this hipcc emitted ONE
+  // buffer_load_dword and splatted it into all four lanes (caught by the parity tests)
+  const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 0);
+  const f32x4 f = __builtin_bit_cast(f32x4, v);
+  return make_float4(f.x, f.y, f.z, f.w);
+}
+
 // LDS read of N consecutive floats with ds_read_b64 (B64) or ds_read_b128.
 template <bool B64, int N>
 __device__ __forceinline__ void lds_read(const float* p, float (&v)[N]) {
@@ -595,6 +613,9 @@ __device__ __forceinline__ void corr_bwd_tile(float* sm, const float* __restrict
   // g of sample b at b * ep.g_bstride: a channel slice of the concat gradient,
   // or the dense [B,K*K,H,W] tensor
   const float* gb = g + (size_t)b * ep.g_bstride;
+  // raw buffer descriptors over this sample's K*K planes: 16-byte loads with a
+  // 32-bit offset (one VGPR per address instead of a 64-bit pointer pair)
+  const auto grs = plane_buf(gb, K * K * HW * 4);
 
   // this wave's DYW rows of g for its PX pixels, read once. All loads are
   // unconditional at clamped in-bounds offsets (no branch, so no wait, inside
@@ -612,27 +633,22 @@ __device__ __forceinline__ void corr_bwd_tile(float* sm, const float* __restrict
     for (int dx = 0; dx < K; ++dx) {
       const int k = min(dy, K - 1) * K + dx;
       const int yy = G2 ? y - dy + D : y;
+      const bool rowok = dy < K && (unsigned)yy < (unsigned)H;
       if constexpr (USF_BWD_VECG && V == 4 && PX % 4 == 0) {
-        const bool rowok = dy < K && (unsigned)yy < (unsigned)H;
-        const float* row = gb + k * HW + (rowok ? yy : 0) * W;
+        const unsigned ro = (unsigned)(k * HW + (rowok ? yy : 0) * W);
 #pragma unroll
         for (int i4 = 0; i4 < PX; i4 += 4) {
           const int xs = G2 ? xb + i4 - dx + D : xb + i4;
           const int xc = min(max(xs, 0), W - 4);
-          float4 v;
-          __builtin_memcpy(&v, row + xc, sizeof(v));
+          const float4 v = buf_load4(grs, (int)((ro + (unsigned)xc) * 4u));
           const int shift = xs - xc;  // 0 inside the image
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             const int xx = xs + i;
             const bool ok = rowok && (unsigned)xx < (unsigned)W;
-            float e;
-            if constexpr (G2) {
-              const int idx = i + shift;
-              e = idx <= 0 ? v.x : idx == 1 ? v.y : idx == 2 ? v.z : v.w;
-            } else {
-              e = i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w;  // gx1 runs are aligned, never shifted
-            }
+            // gx2's edge lanes pick their element by index; gx1 runs are aligned, never shifted
+            const int idx = G2 ? i + shift : i;
+            const float e = idx <= 0 ? v.x : idx == 1 ? v.y : idx == 2 ? v.z : v.w;
             gv[t][dx][i4 + i] = ok ? e : 0.f;
           }
         }
@@ -640,8 +656,8 @@ __device__ __forceinline__ void corr_bwd_tile(float* sm, const float* __restrict
 #pragma unroll
         for (int i = 0; i < PX; ++i) {
           const int xx = G2 ? xb + i - dx + D : xb + i;
-          const bool ok = dy < K && (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W;
-          const float v = gb[k * HW + (ok ? yy * W + xx : 0)];
+          const bool ok = rowok && (unsigned)xx < (unsigned)W;
+          const float v = buf_load1(grs, (k * HW + (ok ? yy * W + xx : 0)) * 4);
           gv[t][dx][i] = ok ? v : 0.f;
         }
       }
@@ -927,6 +943,12 @@ long long corr_fwd_workspace(int B, int C, int H, int W, int d) {
   const long long K = 2 * d + 1;
   return (long long)p.groups * B * K * K * H * W;
 }
+
+// The LeakyReLU derivative is a separate dense pass (leaky_bwd_gather_kernel).
+// Fusing it into the g loads (the forward's activated output loaded at the same
+// offsets, or only its signs packed into bits) spilled 250-600 bytes past the
+// 168-VGPR budget of the 3-waves/SIMD backward in every arrangement tried.
+bool corr_bwd_fuses_act(int, int) { return false; }
 
 hipError_t corr_bwd_launch(const float* x1, const float* x2, const float* gout, float* gx1,
                            float* gx2, int B, int C, int H, int W, int d, hipStream_t s, BwdEpi ep) {

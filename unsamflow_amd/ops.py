@@ -394,17 +394,19 @@ def corr_backward_ex(x1: torch.Tensor, x2: torch.Tensor, grad_out: torch.Tensor,
     K = 2 * d + 1
     gbs = _plane_slice_stride("grad_output", grad_out, (B, K * K, H, W))
     scratch = None
+    lib = _lib.load()
     if act_out is not None:
         _require_device_f32("act_out", act_out)
         if _plane_slice_stride("act_out", act_out, (B, K * K, H, W)) != gbs:
             raise ValueError("act_out and grad_output must share the batch stride")
-        scratch = torch.empty((B, K * K, H, W), device=x1.device, dtype=torch.float32)
+        n = int(lib.usf_corr_bwd_ex_scratch(B, C, H, W, d))
+        if n:
+            scratch = torch.empty(n, device=x1.device, dtype=torch.float32)
     if not (need_x1 or need_x2):
         return None, None
     x1c, x2c = x1.contiguous(), x2.contiguous()
     g1 = torch.empty_like(x1c) if need_x1 else None
     g2 = torch.empty_like(x2c) if need_x2 else None
-    lib = _lib.load()
     # with the LeakyReLU derivative the site also reads the activated output
     # once (what leaky_relu_backward needs): a distinct site, its bytes included
     op = "corr_bwd" if act_out is None else "corr_bwd_leaky"
