@@ -31,6 +31,9 @@
  *   usf_flow_upsample_* <- F.interpolate(flow * k, scale_factor=k, bilinear,
  *                        align_corners=True) of the decoder (pwclite.py:299-301;
  *                        SURVEY §8f row 4)
+ *   usf_convex_upsample_* <- UpFlowNetwork.upsample_flow + its 0.25 mask scale
+ *                        (pwclite.py:148-166, the learned x4 output upsampler;
+ *                        SURVEY §8f row 4)
  *
  * Contract (all entry points):
  *   - Pointers are DEVICE pointers to fp32 NCHW tensors. x/x1/x2/gout/out/gx*
@@ -59,7 +62,7 @@
 extern "C" {
 #endif
 
-#define USF_ABI_VERSION 2
+#define USF_ABI_VERSION 3
 #define USF_EINVAL (-1)
 
 /* padding modes for the warp (flow_warp `pad` argument) */
@@ -207,6 +210,29 @@ int usf_flow_upsample_f32(const float* flow, float* out, int B, int C, int H, in
  * from grad_out [B,C,H*factor,W*factor]. */
 int usf_flow_upsample_bwd_f32(const float* grad_out, float* grad_flow, int B, int C, int H,
                               int W, int factor, void* stream);
+
+/* The learned (convex) x`factor` upsampler of the output flows
+ * (UpFlowNetwork, pwclite.py:148-166; RAFT-style), factor in {2, 4, 8}
+ * (the reference uses 4):
+ *   w   = softmax(mask_scale * mask viewed [B,1,9,f,f,H,W], dim 2)
+ *   out[b,c,f*y+i,f*x+j] = sum_k w[b,k,i,j,y,x] * f * flow[b,c,y+ky-1,x+kx-1]
+ * (k = 3 ky + kx, zero outside the image; mask_scale = 0.25 at :165).
+ * flow: [B,2,H,W] dense; mask: [B,9*f*f,H,W] dense (the convs' raw output);
+ * out: [B,2,f*H,f*W] dense, overwritten. */
+int usf_convex_upsample_f32(const float* flow, const float* mask, float* out, int B, int H, int W,
+                            int factor, float mask_scale, void* stream);
+
+/* Floats of scratch usf_convex_upsample_bwd_f32 needs when grad_flow is wanted
+ * (18 * B * H * W). */
+long long usf_convex_upsample_bwd_scratch(int B, int H, int W);
+
+/* Its backward from grad_out [B,2,f*H,f*W]: grad_flow [B,2,H,W] and grad_mask
+ * [B,9*f*f,H,W] w.r.t. the RAW mask (mask_scale applied), both dense,
+ * overwritten, deterministic (no atomics); either may be NULL. scratch:
+ * usf_convex_upsample_bwd_scratch floats when grad_flow is non-NULL. */
+int usf_convex_upsample_bwd_f32(const float* flow, const float* mask, const float* grad_out,
+                                float* grad_flow, float* grad_mask, float* scratch, int B, int H,
+                                int W, int factor, float mask_scale, void* stream);
 
 /* The loss's image pyramid (unFlowLoss per scale s: F.interpolate(im,
  * (H >> s, W >> s), mode="area"), flow_loss.py:128-129): out_s = mean of each

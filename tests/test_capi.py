@@ -37,6 +37,7 @@ def test_header_declares_the_abi():
          "usf_photo_loss_partials", "usf_photo_loss_fwd_f32", "usf_photo_loss_pair_fwd_f32",
          "usf_photo_loss_bwd_f32",
          "usf_flow_upsample_f32", "usf_flow_upsample_bwd_f32", "usf_area_pyramid_f32",
+         "usf_convex_upsample_f32", "usf_convex_upsample_bwd_scratch", "usf_convex_upsample_bwd_f32",
          "usf_set_variant"]
     )
 
@@ -56,7 +57,7 @@ def test_library_exports_every_declared_symbol(lib):
 def test_abi_version(lib):
     from unsamflow_amd import _lib
 
-    assert lib.usf_abi_version() == _lib.ABI_VERSION == 2
+    assert lib.usf_abi_version() == _lib.ABI_VERSION == 3
 
 
 def test_no_torch_types_in_abi():
@@ -99,6 +100,11 @@ def test_no_torch_types_in_abi():
         (lambda L: L.usf_photo_loss_bwd_f32(1, 1, 1, 1, 0, 4, 4, 1, None), "non-positive"),
         (lambda L: L.usf_photo_loss_bwd_f32(1, 1, 1, 1, 1, 4, 4, 3, None), "ndir=3"),
         (lambda L: L.usf_photo_loss_pair_fwd_f32(1, 1, 1, 1, 1, 32, 1, 1, None, 2, 3, 4, 4, 1, 0.15, 0.85, None), "< 4*H*W"),
+        (lambda L: L.usf_convex_upsample_f32(1, 1, 1, 2, 4, 4, 3, 0.25, None), "factor 3"),
+        (lambda L: L.usf_convex_upsample_f32(1, None, 1, 2, 4, 4, 4, 0.25, None), "null pointer"),
+        (lambda L: L.usf_convex_upsample_f32(1, 1, 1, 2, 0, 4, 4, 0.25, None), "non-positive"),
+        (lambda L: L.usf_convex_upsample_bwd_f32(1, 1, 1, 1, 1, None, 2, 4, 4, 4, 0.25, None), "needs scratch"),
+        (lambda L: L.usf_convex_upsample_bwd_f32(1, 1, None, 1, 1, 1, 2, 4, 4, 4, 0.25, None), "null input"),
         (lambda L: L.usf_photo_loss_pair_fwd_f32(1, 1, 1, None, 1, 64, 1, 1, None, 2, 3, 4, 4, 1, 0.15, 0.85, None), "null input"),
     ],
 )

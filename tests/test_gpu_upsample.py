@@ -42,3 +42,66 @@ def test_area_pyramid_bit_exact_vs_torch_cpu(hip_device, B, C, H, W):
     for s, o in zip((1, 2, 3), outs):
         ref = F.interpolate(x, (H >> s, W >> s), mode="area")
         assert torch.equal(o.cpu(), ref), (s, float((o.cpu() - ref).abs().max()))
+
+
+@pytest.mark.parametrize("B,H,W,f", [(2, 5, 7, 4), (1, 1, 1, 4), (8, 4, 13, 4), (2, 64, 208, 4), (3, 9, 70, 4),
+                                     (1, 6, 9, 2), (1, 3, 5, 8)])
+def test_convex_upsample_matches_oracle(hip_device, B, H, W, f):
+    """usf_convex_upsample_{f32,bwd_f32} vs oracle/upsample.py (UpFlowNetwork,
+    pwclite.py:140-166): fp32 kernel vs fp64 oracle, atol 1e-4 + rtol 1e-5 on
+    outputs of magnitude ~100."""
+    from oracle.upsample import convex_upsample_backward_np, convex_upsample_np
+    from unsamflow_amd.upsample import convex_upsample
+
+    flow = hashrng.symmetric((B, 2, H, W), 400 + H, 20.0)
+    mask = hashrng.normal((B, 9 * f * f, H, W), 401 + W) * np.float32(3.0)
+    gout = hashrng.normal((B, 2, f * H, f * W), 402)
+    fd = torch.from_numpy(flow).to(hip_device).requires_grad_(True)
+    md = torch.from_numpy(mask).to(hip_device).requires_grad_(True)
+    out = convex_upsample(fd, md, f, 0.25)
+    out.backward(torch.from_numpy(gout).to(hip_device))
+    np.testing.assert_allclose(out.detach().cpu().numpy(), convex_upsample_np(flow, mask, f, 0.25),
+                               atol=1e-4, rtol=1e-5)
+    gf, gm = convex_upsample_backward_np(flow, mask, gout, f, 0.25)
+    np.testing.assert_allclose(fd.grad.cpu().numpy(), gf, atol=1e-4, rtol=1e-5)
+    np.testing.assert_allclose(md.grad.cpu().numpy(), gm, atol=1e-4, rtol=1e-5)
+
+
+def test_convex_upsample_deterministic_and_partial_grads(hip_device):
+    from unsamflow_amd import ops
+
+    B, H, W, f = 2, 64, 208, 4
+    flow = torch.from_numpy(hashrng.symmetric((B, 2, H, W), 410, 20.0)).to(hip_device)
+    mask = torch.from_numpy(hashrng.normal((B, 144, H, W), 411)).to(hip_device)
+    go = torch.from_numpy(hashrng.normal((B, 2, f * H, f * W), 412)).to(hip_device)
+    a = ops.convex_upsample_backward(flow, mask, go, f)
+    b = ops.convex_upsample_backward(flow, mask, go, f)
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+    gf, gm = ops.convex_upsample_backward(flow, mask, go, f, need_mask=False)
+    assert gm is None and torch.equal(gf, a[0])
+    gf, gm = ops.convex_upsample_backward(flow, mask, go, f, need_flow=False)
+    assert gf is None and torch.equal(gm, a[1])
+
+
+def test_upflow_network_fused_matches_torch_form(hip_device):
+    """The model's UpFlowNetwork with the HIP op vs its torch form (pwclite.py:
+    148-166) on the device, including the convs' parameter gradients."""
+    from unsamflow_amd.pwclite import UpFlowNetwork
+
+    torch.manual_seed(0)
+    net = UpFlowNetwork(96, 4).to(hip_device)
+    flow = torch.randn(2, 2, 16, 52, device=hip_device) * 5
+    feat = torch.randn(2, 96, 16, 52, device=hip_device)
+    go = torch.randn(2, 2, 64, 208, device=hip_device)
+    outs, grads = [], []
+    for fused in (False, True):
+        net.fused = fused
+        net.zero_grad()
+        fl = flow.clone().requires_grad_(True)
+        out = net(fl, feat)
+        out.backward(go)
+        outs.append(out.detach())
+        grads.append([fl.grad] + [p.grad.clone() for p in net.parameters()])
+    torch.testing.assert_close(outs[1], outs[0], atol=1e-4, rtol=1e-5)
+    for a, b in zip(grads[1], grads[0]):
+        torch.testing.assert_close(a, b, atol=2e-3, rtol=1e-4)

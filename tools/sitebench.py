@@ -37,6 +37,8 @@ def site_list(ops):
             out += [(op, (8, 2, H, W)) for H, W in SCALES]
         elif op == "occ_bwd":
             out += [(op, (8, 1, 256, 832))]
+        elif op in ("convex_up", "convex_up_bwd"):
+            out += [(op, (8, H, W, 4)) for _, H, W in KITTI]
         elif op == "area_pyramid":
             out += [(op, (8, 3, 256, 832))]
         elif op in ("upsample", "upsample_bwd"):
@@ -50,6 +52,10 @@ def alg_bytes(op, key):
     if op == "photo_bwd":
         B, ndir, H, W = key
         return 4 * B * H * W * 6 * ndir
+    if op in ("convex_up", "convex_up_bwd"):
+        B, H, W, f = key  # flow + mask read, out written; backward adds grad_out, grad_flow, grad_mask
+        ff = f * f
+        return 4 * B * H * W * ((2 + 11 * ff) if op == "convex_up" else (4 + 20 * ff))
     B, C, H, W = key[:4]
     if op == "corr_fwd":
         return 4 * B * H * W * (2 * C + 81)

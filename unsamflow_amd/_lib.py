@@ -17,7 +17,7 @@ from pathlib import Path
 import torch  # noqa: F401  (load torch's HIP runtime before the plugin)
 
 _LIB_PATH = Path(os.environ.get("USF_LIB", Path(__file__).resolve().parent / "lib" / "libunsamflow_hip.so"))
-ABI_VERSION = 2
+ABI_VERSION = 3
 PAD_ZEROS = 0
 PAD_BORDER = 1
 
@@ -81,6 +81,15 @@ _SIGNATURES = {
     ),
     "usf_flow_upsample_f32": ([_c_float_p] * 2 + [ctypes.c_int] * 5 + [ctypes.c_void_p], ctypes.c_int),
     "usf_flow_upsample_bwd_f32": ([_c_float_p] * 2 + [ctypes.c_int] * 5 + [ctypes.c_void_p], ctypes.c_int),
+    "usf_convex_upsample_f32": (
+        [_c_float_p] * 3 + [ctypes.c_int] * 4 + [ctypes.c_float, ctypes.c_void_p],
+        ctypes.c_int,
+    ),
+    "usf_convex_upsample_bwd_scratch": ([ctypes.c_int] * 3, ctypes.c_longlong),
+    "usf_convex_upsample_bwd_f32": (
+        [_c_float_p] * 6 + [ctypes.c_int] * 4 + [ctypes.c_float, ctypes.c_void_p],
+        ctypes.c_int,
+    ),
     "usf_area_pyramid_f32": ([_c_float_p] * 4 + [ctypes.c_int] * 4 + [ctypes.c_void_p], ctypes.c_int),
     "usf_set_variant": ([ctypes.c_int, ctypes.c_int], ctypes.c_int),
 }

@@ -23,7 +23,7 @@ INCLUDE_DIR = PKG_DIR.parent / "include"
 ARCH = os.environ.get("USF_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
-SOURCES = ["corr.hip", "warp.hip", "photo.hip", "upsample.hip", "capi.cpp"]
+SOURCES = ["corr.hip", "warp.hip", "photo.hip", "upsample.hip", "convex.hip", "capi.cpp"]
 HEADERS = ["usf_common.h", "warp_tap.h"]
 
 # -fno-slp-vectorize: the SLP vectorizer packs the kernels' independent FMAs into

@@ -407,6 +407,60 @@ int usf_flow_upsample_bwd_f32(const float* grad_out, float* grad_flow, int B, in
                 (hipStream_t)stream);
 }
 
+static bool check_convex(const char* fn, int B, int H, int W, int factor) {
+  if (!check_dims(fn, B, 2, H, W)) return false;
+  if (!convex_factor_ok(factor)) {
+    set_error("%s: factor %d (2, 4 or 8)", fn, factor);
+    return false;
+  }
+  if ((long long)9 * factor * factor * H * W > 0x1FFFFFFFLL) {
+    set_error("%s: mask plane block too large", fn);
+    return false;
+  }
+  return true;
+}
+
+int usf_convex_upsample_f32(const float* flow, const float* mask, float* out, int B, int H, int W,
+                            int factor, float mask_scale, void* stream) {
+  clear_error();
+  const char* fn = "usf_convex_upsample_f32";
+  if (!check_convex(fn, B, H, W, factor)) return USF_EINVAL;
+  if (!flow || !mask || !out) {
+    set_error("%s: null pointer", fn);
+    return USF_EINVAL;
+  }
+  if (const int pe = pre_check(fn, (hipStream_t)stream)) return pe;
+  return finish(fn, convex_fwd_launch(flow, mask, out, B, H, W, factor, mask_scale, (hipStream_t)stream),
+                (hipStream_t)stream);
+}
+
+long long usf_convex_upsample_bwd_scratch(int B, int H, int W) {
+  if (B < 0 || H < 0 || W < 0) return 0;
+  return convex_bwd_scratch(B, H, W);
+}
+
+int usf_convex_upsample_bwd_f32(const float* flow, const float* mask, const float* grad_out,
+                                float* grad_flow, float* grad_mask, float* scratch, int B, int H,
+                                int W, int factor, float mask_scale, void* stream) {
+  clear_error();
+  const char* fn = "usf_convex_upsample_bwd_f32";
+  if (!check_convex(fn, B, H, W, factor)) return USF_EINVAL;
+  if (!flow || !mask || !grad_out) {
+    set_error("%s: null input pointer", fn);
+    return USF_EINVAL;
+  }
+  if (grad_flow && !scratch) {
+    set_error("%s: grad_flow needs scratch (usf_convex_upsample_bwd_scratch floats)", fn);
+    return USF_EINVAL;
+  }
+  if (!grad_flow && !grad_mask) return 0;
+  if (const int pe = pre_check(fn, (hipStream_t)stream)) return pe;
+  return finish(fn,
+                convex_bwd_launch(flow, mask, grad_out, grad_flow, grad_mask, scratch, B, H, W, factor,
+                                  mask_scale, (hipStream_t)stream),
+                (hipStream_t)stream);
+}
+
 int usf_area_pyramid_f32(const float* x, float* out1, float* out2, float* out3, int B, int C, int H,
                          int W, void* stream) {
   clear_error();

@@ -109,6 +109,13 @@ hipError_t upsample_fwd_launch(const float* x, float* out, int B, int C, int H, 
                                hipStream_t s);
 hipError_t upsample_bwd_launch(const float* gout, float* gx, int B, int C, int H, int W, int k,
                                hipStream_t s);
+bool convex_factor_ok(int factor);
+long long convex_bwd_scratch(int B, int H, int W);
+hipError_t convex_fwd_launch(const float* flow, const float* mask, float* out, int B, int H, int W,
+                             int factor, float mask_scale, hipStream_t s);
+hipError_t convex_bwd_launch(const float* flow, const float* mask, const float* gout, float* gflow,
+                             float* gmask, float* scratch, int B, int H, int W, int factor,
+                             float mask_scale, hipStream_t s);
 hipError_t area_pyramid_launch(const float* x, float* o1, float* o2, float* o3, long long planes,
                                int H, int W, hipStream_t s);
 

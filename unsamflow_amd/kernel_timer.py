@@ -170,6 +170,14 @@ def site_launcher(op: str, key, device, seed: int = 0):
             return lambda: ops.flow_upsample(f, k)
         go = torch.randn(B, C, H * k, W * k, device=device, generator=g)
         return lambda: ops.flow_upsample_backward(go, k)
+    if op in ("convex_up", "convex_up_bwd"):
+        B, H, W, f = key
+        flow = torch.randn(B, 2, H, W, device=device, generator=g)
+        mask = torch.randn(B, 9 * f * f, H, W, device=device, generator=g)
+        if op == "convex_up":
+            return lambda: ops.convex_upsample(flow, mask, f)
+        go = torch.randn(B, 2, f * H, f * W, device=device, generator=g)
+        return lambda: ops.convex_upsample_backward(flow, mask, go, f)
     if op == "area_pyramid":
         img = torch.rand(*key, device=device, generator=g)
         return lambda: ops.area_pyramid(img)

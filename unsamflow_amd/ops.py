@@ -458,6 +458,55 @@ def flow_upsample_backward(grad_out: torch.Tensor, factor: int) -> torch.Tensor:
     return gx
 
 
+def convex_upsample(flow: torch.Tensor, mask: torch.Tensor, factor: int = 4,
+                    mask_scale: float = 0.25) -> torch.Tensor:
+    """UpFlowNetwork.upsample_flow(flow, mask_scale * mask) (pwclite.py:148-166):
+    flow [B,2,H,W], mask [B,9*f*f,H,W] (the convs' raw output) -> [B,2,fH,fW]."""
+    _require_device_f32("flow", flow)
+    _require_device_f32("mask", mask)
+    B, C, H, W = _nchw("flow", flow)
+    f = int(factor)
+    if C != 2 or tuple(mask.shape) != (B, 9 * f * f, H, W):
+        raise ValueError(f"convex_upsample: flow {tuple(flow.shape)} / mask {tuple(mask.shape)} (want [B,2,H,W] / "
+                         f"[B,{9 * f * f},H,W])")
+    fc, mc = flow.contiguous(), mask.contiguous()
+    out = torch.empty((B, 2, f * H, f * W), device=flow.device, dtype=torch.float32)
+    lib = _lib.load()
+    nbytes = 4 * B * H * W * (2 + 11 * f * f)
+    with torch.cuda.device(flow.device), _kt.timed("convex_up", (B, H, W, f), flow.device, nbytes):
+        rc = lib.usf_convex_upsample_f32(fc.data_ptr(), mc.data_ptr(), out.data_ptr(), B, H, W, f,
+                                         float(mask_scale), _lib.stream_handle(flow.device))
+    _lib.check(rc, "usf_convex_upsample_f32")
+    return out
+
+
+def convex_upsample_backward(flow: torch.Tensor, mask: torch.Tensor, grad_out: torch.Tensor, factor: int = 4,
+                             mask_scale: float = 0.25, need_flow: bool = True, need_mask: bool = True):
+    """(grad_flow, grad_mask) of convex_upsample; grad_mask is w.r.t. the raw mask."""
+    _require_device_f32("grad_out", grad_out)
+    B, _, H, W = _nchw("flow", flow)
+    f = int(factor)
+    if tuple(grad_out.shape) != (B, 2, f * H, f * W):
+        raise ValueError(f"convex_upsample_backward: grad_out {tuple(grad_out.shape)}")
+    if not (need_flow or need_mask):
+        return None, None
+    fc, mc, gc = flow.contiguous(), mask.contiguous(), grad_out.contiguous()
+    gf = torch.empty((B, 2, H, W), device=flow.device, dtype=torch.float32) if need_flow else None
+    gm = torch.empty_like(mc) if need_mask else None
+    lib = _lib.load()
+    scratch = None
+    if need_flow:
+        scratch = torch.empty(int(lib.usf_convex_upsample_bwd_scratch(B, H, W)), device=flow.device,
+                              dtype=torch.float32)
+    nbytes = 4 * B * H * W * (2 + 9 * f * f + 2 * f * f + (2 if need_flow else 0) + (9 * f * f if need_mask else 0))
+    with torch.cuda.device(flow.device), _kt.timed("convex_up_bwd", (B, H, W, f), flow.device, nbytes):
+        rc = lib.usf_convex_upsample_bwd_f32(fc.data_ptr(), mc.data_ptr(), gc.data_ptr(), _ptr(gf), _ptr(gm),
+                                             _ptr(scratch), B, H, W, f, float(mask_scale),
+                                             _lib.stream_handle(flow.device))
+    _lib.check(rc, "usf_convex_upsample_bwd_f32")
+    return gf, gm
+
+
 def area_pyramid(x: torch.Tensor):
     """The loss's image pyramid: ``[F.interpolate(x, (H >> s, W >> s), mode="area")
     for s in 1, 2, 3]`` (flow_loss.py:128-129), one read of x, bit-exact with

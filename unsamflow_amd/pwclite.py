@@ -128,6 +128,7 @@ class UpFlowNetwork(nn.Module):
     def __init__(self, ch_in: int = 96, scale_factor: int = 4):
         super().__init__()
         self.scale = scale_factor
+        self.fused = False  # PWCLite turns on the HIP op (csrc/convex.hip) with its own corr/warp
         self.convs = nn.Sequential(conv_block(ch_in, 128, 3, 1, 1), conv_block(128, scale_factor ** 2 * 9, 3, 1, 1))
 
     def upsample_flow(self, flow, mask):
@@ -139,6 +140,10 @@ class UpFlowNetwork(nn.Module):
         return up.permute(0, 1, 4, 2, 5, 3).reshape(N, 2, s * H, s * W)
 
     def forward(self, flow, feat):
+        if self.fused and flow.is_cuda:
+            from .upsample import convex_upsample
+
+            return convex_upsample(flow, self.convs(feat), self.scale, 0.25)
         return self.upsample_flow(flow, 0.25 * self.convs(feat))
 
 
@@ -181,6 +186,8 @@ class PWCLite(nn.Module):
         self.flow_estimators = (FlowEstimatorReduce if cfg.reduce_dense else FlowEstimatorDense)(self.num_ch_in)
         self.context_networks = ContextNetwork(self.flow_estimators.feat_dim + 2)
         self.output_flow_upsampler = UpFlowNetwork(ch_in=96, scale_factor=4) if cfg.learned_upsampler else None
+        if self.output_flow_upsampler is not None:
+            self.output_flow_upsampler.fused = self.fused_corr_cat
         # 1x1 projections of the decoder levels' features (192, 128, 96, 64, 32 channels)
         level_chs = self.num_chs[::-1][:5]
         self.conv_1x1 = nn.ModuleList([conv_block(c, 32, k=1) for c in level_chs])
