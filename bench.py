@@ -2,8 +2,10 @@
 """Benchmark: image-pairs/sec of one PWCLite training step, KITTI 832x256, d=4.
 
 A step (unsamflow_amd.harness.TrainStep) is the reference trainer's step:
-PWCLite fwd with_bk (10 correlation + 8 decoder-warp calls through the HIP
-library) -> unFlowLoss (8 loss warps) -> backward -> clip_grad_norm_ -> Adam ->
+PWCLite fwd with_bk (both directions stacked on the batch: 5 correlation + 4
+decoder-warp calls at batch 16 through the HIP library; --per-direction: the
+reference's two batch-8 passes) -> unFlowLoss (8 loss warps) -> backward ->
+clip_grad_norm_ -> Adam ->
 OneCycleLR, on B=8 synthetic U[0,1) frame pairs per GPU (kitti_base.json),
 random-init weights. N>1: one process per GPU (torchrun), DDP over RCCL
 ("nccl"), B=8 per rank (weak scaling).
@@ -71,6 +73,9 @@ def parse():
                     help="skip the graph-replay device times (keeps a rocprofv3 run to real steps only)")
     ap.add_argument("--cudnn-benchmark", action="store_true",
                     help="MIOpen find-mode tuning of the convolutions (slow first steps)")
+    ap.add_argument("--per-direction", action="store_true",
+                    help="run with_bk as the reference's two batch-B passes instead of one batch-2B pass "
+                         "(PWCLite.batch_directions = False)")
     ap.add_argument("--graph", action="store_true",
                     help="replay the step from HIP graphs (harness.GraphedTrainStep); measured equal to "
                          "eager at N=1 (the step is GPU-bound), so eager is the default")
@@ -260,6 +265,7 @@ def main():
     # graph mode: the whole step is captured once and replayed (harness.GraphedTrainStep);
     # data parallel = one all-reduce of the flat gradient buffer between the two graphs
     step = TrainStep(cfg, device, ddp=distributed and not use_graph, seed=42 + rank, capturable=use_graph)
+    step.module.batch_directions = not args.per_direction
     img1, img2, s1, s2 = synthetic_pair(args.batch, c["H"], c["W"], device, seed=42 + rank,
                                         with_seg=args.config != "kitti")
 

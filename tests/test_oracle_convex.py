@@ -8,6 +8,7 @@ first test captures the upsampler's inputs inside that golden run and checks
 that the oracle reproduces the reference's flows from them; the second checks
 the oracle's backward against autograd of its forward (float64)."""
 import numpy as np
+import pytest
 import torch
 
 from conftest import load_golden
@@ -18,24 +19,33 @@ from unsamflow_amd.config import AttrDict, kitti_base
 from unsamflow_amd.pwclite import PWCLite, UpFlowNetwork
 
 
-def test_convex_oracle_reproduces_reference_flows():
+@pytest.mark.parametrize("batched", [False, True])
+def test_convex_oracle_reproduces_reference_flows(batched):
     z = load_golden("pwclite_kitti.npz")
     cfg = kitti_base()
     assert cfg.model.learned_upsampler
     model = PWCLite(AttrDict.wrap(dict(cfg.model)), corr_module=OracleCorrelation(4), warp_fn=oracle_flow_warp)
     hash_init_(model, seed=1)
+    model.batch_directions = batched
     up = model.output_flow_upsampler
     calls = []
     up.register_forward_hook(lambda m, inp, out: calls.append((inp[0].detach(), inp[1].detach())))
     with torch.no_grad():
         model(torch.from_numpy(z["img1"]), torch.from_numpy(z["img2"]), with_bk=True)
-    assert len(calls) == 10  # 5 levels x 2 directions
+    # 5 levels x 2 directions, or 5 levels with both directions stacked on the batch
+    assert len(calls) == (5 if batched else 10)
+    B = z["img1"].shape[0]
     for j, (flow, feat) in enumerate(calls):
         with torch.no_grad():
             mask = up.convs(feat).numpy()
         got = convex_upsample_np(flow.numpy(), mask, 4, 0.25)
-        key = f"flow{'12' if j < 5 else '21'}_{4 - j % 5}"  # the decoder returns flows[::-1]
-        np.testing.assert_allclose(got, z[key], atol=1e-5, rtol=1e-4, err_msg=key)
+        lvl = 4 - j % 5  # the decoder returns flows[::-1]
+        if batched:
+            pairs = [(got[:B], f"flow12_{lvl}"), (got[B:], f"flow21_{lvl}")]
+        else:
+            pairs = [(got, f"flow{'12' if j < 5 else '21'}_{lvl}")]
+        for arr, key in pairs:
+            np.testing.assert_allclose(arr, z[key], atol=1e-5, rtol=1e-4, err_msg=key)
 
 
 def test_convex_oracle_backward_is_the_gradient():

@@ -1,4 +1,6 @@
-"""Launch each hot-path kernel N times at PWCLite's B=8 KITTI call-site shapes,
+"""Launch each hot-path kernel N times at PWCLite's KITTI call-site shapes (B=8
+pairs: the decoder's sites at batch 16 = both with_bk directions stacked,
+PWCLite.batch_directions; the loss's at 8),
 plain (no graphs) so rocprofv3 --pmc attributes counters per dispatch.
 Usage: rocprofv3 --pmc <counters> --kernel-trace --output-format csv -d DIR -o run -- python3 tools/kprof.py
 """
@@ -12,14 +14,17 @@ from unsamflow_amd import _lib  # noqa: E402
 from unsamflow_amd.kernel_timer import site_launcher  # noqa: E402
 
 KITTI = [(192, 4, 13), (128, 8, 26), (96, 16, 52), (64, 32, 104), (32, 64, 208)]
-SITES = [("corr_fwd", (8, C, H, W)) for C, H, W in KITTI]
-SITES += [("corr_bwd", (8, C, H, W, True, True)) for C, H, W in KITTI]
+DB = int(os.environ.get("KPROF_DECODER_B", "16"))  # decoder batch: 2 x 8 pairs
+SITES = [("corr_fwd", (DB, C, H, W)) for C, H, W in KITTI]
+SITES += [("corr_bwd", (DB, C, H, W, True, True)) for C, H, W in KITTI]
 # one direction at a time (where the backward's traffic comes from)
-SITES += [("corr_bwd", (8, C, H, W, n1, not n1)) for C, H, W in KITTI[3:] for n1 in (True, False)]
-SITES += [("corr_bwd_leaky", (8, C, H, W, True, True)) for C, H, W in KITTI]
-SITES += [("warp_fwd", (8, C, H, W, "border")) for C, H, W in KITTI[1:]]
-SITES += [("warp_bwd", (8, C, H, W, "border", True, True)) for C, H, W in KITTI[1:]]
+SITES += [("corr_bwd", (DB, C, H, W, n1, not n1)) for C, H, W in KITTI[3:] for n1 in (True, False)]
+SITES += [("corr_bwd_leaky", (DB, C, H, W, True, True)) for C, H, W in KITTI]
+SITES += [("warp_fwd", (DB, C, H, W, "border")) for C, H, W in KITTI[1:]]
+SITES += [("warp_bwd", (DB, C, H, W, "border", True, True)) for C, H, W in KITTI[1:]]
 SITES += [("warp_fwd", (8, 3, 256, 832, "border")), ("warp_bwd", (8, 3, 256, 832, "border", False, True))]
+SITES += [("convex_up", (DB, H, W, 4)) for _, H, W in KITTI]
+SITES += [("convex_up_bwd", (DB, H, W, 4)) for _, H, W in KITTI]
 SITES += [("occ_bwd", (8, 1, 256, 832)), ("area_pyramid", (8, 3, 256, 832))]
 SITES += [("photo_fwd", (8, 3, 256 >> i, 832 >> i, "border")) for i in range(4)]
 SITES += [("photo_fwd_grad", (8, 3, 256 >> i, 832 >> i, "border")) for i in range(4)]

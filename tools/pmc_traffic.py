@@ -57,7 +57,8 @@ def main():
     uf = [v for name, v in fetch if "usf::" in name]
     uw = [v for name, v in write if "usf::" in name]
     # library kernels per launch of a site (summed): splat + threshold, partials + final
-    per_launch = {"occ_bwd": 2, "photo_fwd": 2, "photo_fwd_grad": 2, "photo_pair_grad": 2, "corr_bwd_leaky": 2}
+    per_launch = {"occ_bwd": 2, "photo_fwd": 2, "photo_fwd_grad": 2, "photo_pair_grad": 2, "corr_bwd_leaky": 2,
+                  "convex_up_bwd": 2}
     # kernels a site's launcher runs once before its timed launches
     prefix = {}
     sites, pos = [], 0
@@ -74,12 +75,18 @@ def main():
         pos += k * n
         if op == "photo_bwd":
             B, ndir, H, W = key
+        elif op.startswith("convex_up"):
+            B, H, W, f = key
         else:
             B, C, H, W = key[:4]
         if op.startswith("corr"):
             alg = corr_bytes(*key[:4], backward=op.startswith("corr_bwd"))
             if op == "corr_bwd_leaky":
                 alg += 4 * B * H * W * 81  # the activated output read by the LeakyReLU derivative
+        elif op == "convex_up":
+            alg = 4 * B * H * W * (2 + 11 * f * f)
+        elif op == "convex_up_bwd":
+            alg = 4 * B * H * W * (4 + 20 * f * f)
         elif op == "warp_fwd":
             alg = warp_bytes(*key[:4])
         elif op == "warp_bwd":

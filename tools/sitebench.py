@@ -18,19 +18,20 @@ from unsamflow_amd.kernel_timer import device_time_us, site_launcher  # noqa: E4
 
 KITTI = [(192, 4, 13), (128, 8, 26), (96, 16, 52), (64, 32, 104), (32, 64, 208)]
 SCALES = [(256 >> i, 832 >> i) for i in range(4)]
+DB = int(os.environ.get("SITEBENCH_DECODER_B", "16"))  # decoder sites: both with_bk directions stacked
 
 
 def site_list(ops):
     out = []
     for op in ops:
         if op == "corr_fwd":
-            out += [(op, (8, C, H, W)) for C, H, W in KITTI]
+            out += [(op, (DB, C, H, W)) for C, H, W in KITTI]
         elif op in ("corr_bwd", "corr_bwd_leaky"):
-            out += [(op, (8, C, H, W, True, True)) for C, H, W in KITTI]
+            out += [(op, (DB, C, H, W, True, True)) for C, H, W in KITTI]
         elif op == "warp_fwd":
-            out += [(op, (8, C, H, W, "border")) for C, H, W in KITTI[1:]]
+            out += [(op, (DB, C, H, W, "border")) for C, H, W in KITTI[1:]]
         elif op == "warp_bwd":
-            out += [(op, (8, C, H, W, "border", True, True)) for C, H, W in KITTI[1:]]
+            out += [(op, (DB, C, H, W, "border", True, True)) for C, H, W in KITTI[1:]]
         elif op in ("photo_fwd", "photo_fwd_grad", "photo_pair", "photo_pair_grad"):
             out += [(op, (8, 3, H, W, "border")) for H, W in SCALES]
         elif op == "photo_bwd":
@@ -38,7 +39,7 @@ def site_list(ops):
         elif op == "occ_bwd":
             out += [(op, (8, 1, 256, 832))]
         elif op in ("convex_up", "convex_up_bwd"):
-            out += [(op, (8, H, W, 4)) for _, H, W in KITTI]
+            out += [(op, (DB, H, W, 4)) for _, H, W in KITTI]
         elif op == "area_pyramid":
             out += [(op, (8, 3, 256, 832))]
         elif op in ("upsample", "upsample_bwd"):
