@@ -47,3 +47,34 @@ def test_corr_leaky_cat_matches_composition(hip_device, B, C, H, W, n_pairs):
     np.testing.assert_array_equal(out.detach().cpu().numpy(), ref.detach().cpu().numpy())
     for a, b in zip(got, want):
         np.testing.assert_allclose(a.cpu().numpy(), b.cpu().numpy(), atol=1e-6, rtol=1e-6)
+
+
+@pytest.mark.parametrize("B,C,H,W", [(2, 32, 64, 208), (2, 64, 32, 104), (8, 96, 16, 52), (1, 8, 5, 4), (3, 16, 7, 12)])
+def test_sign_mask_derivative_equals_dense_pass(hip_device, B, C, H, W):
+    """The forward's LeakyReLU sign mask (epilogue, or the mask kernel after the
+    channel-split reduce at (8, 96, 16, 52)) equals (activated output > 0) bit
+    for bit, and the backward that applies the derivative from it inside its
+    gradient loads gives the same gradients, bit for bit, as the dense
+    derivative pass over the activated output."""
+    from unsamflow_amd import ops
+
+    x1 = torch.from_numpy(hashrng.normal((B, C, H, W), 301)).to(hip_device)
+    x2 = torch.from_numpy(hashrng.normal((B, C, H, W), 302)).to(hip_device)
+    buf = torch.zeros((B, 81 + 34, H, W), device=hip_device)
+    out = buf[:, :81]
+    mask = ops.corr_act_mask(B, H, W, 4, hip_device)
+    assert mask is not None and tuple(mask.shape) == (B, 9, H, W // 4)
+    ops.corr_forward_ex(x1, x2, 4, out, 0.1, act_mask=mask)
+    # expected words from the activated output: bit 4 dx + x % 4 of word (b, dy, y, x // 4)
+    pos = (out > 0).view(B, 9, 9, H, W // 4, 4).to(torch.int64)  # b, dy, dx, y, quad, i
+    shifts = (4 * torch.arange(9, device=hip_device).view(1, 1, 9, 1, 1, 1)
+              + torch.arange(4, device=hip_device).view(1, 1, 1, 1, 1, 4))
+    want = (pos << shifts).sum(dim=(2, 5))
+    assert torch.equal(mask, want)
+    g = torch.from_numpy(hashrng.normal((B, 81 + 34, H, W), 303)).to(hip_device)[:, :81]
+    a1, a2 = ops.corr_backward_ex(x1, x2, g, 4, act_out=out, leaky_slope=0.1)
+    m1, m2 = ops.corr_backward_ex(x1, x2, g, 4, act_out=out, leaky_slope=0.1, act_mask=mask)
+    assert torch.equal(a1, m1) and torch.equal(a2, m2)
+    n1, _ = ops.corr_backward_ex(x1, x2, g, 4, need_x2=False, act_mask=mask, leaky_slope=0.1)
+    _, n2 = ops.corr_backward_ex(x1, x2, g, 4, need_x1=False, act_mask=mask, leaky_slope=0.1)
+    assert torch.equal(n1, a1) and torch.equal(n2, a2)

@@ -35,14 +35,16 @@ _SIGNATURES = {
         ctypes.c_int,
     ),
     "usf_corr_fwd_ex_f32": (
-        [_c_float_p] * 3 + [ctypes.c_longlong, ctypes.c_int, ctypes.c_float, _c_float_p, ctypes.c_longlong]
+        [_c_float_p] * 3 + [ctypes.c_longlong, ctypes.c_int, ctypes.c_float, ctypes.c_void_p, _c_float_p,
+                             ctypes.c_longlong]
         + [ctypes.c_int] * 5 + [ctypes.c_void_p],
         ctypes.c_int,
     ),
+    "usf_corr_act_mask_words": ([ctypes.c_int] * 4, ctypes.c_longlong),
     "usf_corr_fwd_workspace": ([ctypes.c_int] * 5, ctypes.c_longlong),
     "usf_corr_bwd_ex_scratch": ([ctypes.c_int] * 5, ctypes.c_longlong),
     "usf_corr_bwd_ex_f32": (
-        [_c_float_p] * 3 + [ctypes.c_longlong, _c_float_p, ctypes.c_float] + [_c_float_p] * 3
+        [_c_float_p] * 3 + [ctypes.c_longlong, _c_float_p, ctypes.c_void_p, ctypes.c_float] + [_c_float_p] * 3
         + [ctypes.c_int] * 5 + [ctypes.c_void_p],
         ctypes.c_int,
     ),

@@ -7,8 +7,10 @@ as one autograd op. The correlation kernel writes LeakyReLU(corr) straight
 into its channel slice of the concat buffer (usf_corr_fwd_ex_f32: output batch
 stride + activation epilogue), so the 81-channel cost map is neither written
 twice (activation pass) nor copied (cat). Backward reads its gradient from the
-concat gradient's slice (batch stride) and applies the LeakyReLU derivative in
-one dense pass (usf_corr_bwd_ex_f32); the extras' gradients are views.
+concat gradient's slice (batch stride) and applies the LeakyReLU derivative:
+from the sign mask the forward's epilogue wrote (W % 4 == 0: inside the
+backward kernel's gradient loads, no extra pass), else in one dense pass over
+the activated output (usf_corr_bwd_ex_f32); the extras' gradients are views.
 """
 from __future__ import annotations
 
@@ -28,21 +30,26 @@ class CorrLeakyCatFunction(Function):
         ctot = K2 * n_pairs + sum(e.shape[1] for e in extras)
         buf = torch.empty((B, ctot, H, W), device=pairs[0][0].device, dtype=torch.float32)
         off = 0
+        masks = []
         for a, b in pairs:
-            ops.corr_forward_ex(a, b, max_displacement, buf[:, off:off + K2], slope)
+            m = ops.corr_act_mask(B, H, W, max_displacement, a.device)
+            ops.corr_forward_ex(a, b, max_displacement, buf[:, off:off + K2], slope, act_mask=m)
+            masks.append(m)
             off += K2
         for e in extras:
             buf[:, off:off + e.shape[1]].copy_(e)
             off += e.shape[1]
         ctx.md, ctx.slope, ctx.n_pairs, ctx.k2 = max_displacement, slope, n_pairs, K2
         ctx.extra_ch = [e.shape[1] for e in extras]
-        ctx.save_for_backward(*[t for p in pairs for t in p], buf)
+        ctx.has_mask = masks[0] is not None
+        ctx.save_for_backward(*[t for p in pairs for t in p], *(masks if ctx.has_mask else []), buf)
         return buf
 
     @staticmethod
     def backward(ctx, gbuf):
         saved = ctx.saved_tensors
         buf = saved[-1]
+        masks = saved[2 * ctx.n_pairs:2 * ctx.n_pairs + ctx.n_pairs] if ctx.has_mask else [None] * ctx.n_pairs
         grads = []
         off = 0
         gbuf = gbuf if gbuf.is_contiguous() else gbuf.contiguous()
@@ -51,7 +58,8 @@ class CorrLeakyCatFunction(Function):
             need_a = ctx.needs_input_grad[3 + 2 * i]
             need_b = ctx.needs_input_grad[4 + 2 * i]
             ga, gb = ops.corr_backward_ex(a, b, gbuf[:, off:off + ctx.k2], ctx.md, need_a, need_b,
-                                          act_out=buf[:, off:off + ctx.k2], leaky_slope=ctx.slope)
+                                          act_out=buf[:, off:off + ctx.k2], leaky_slope=ctx.slope,
+                                          act_mask=masks[i])
             grads += [ga, gb]
             off += ctx.k2
         for c in ctx.extra_ch:

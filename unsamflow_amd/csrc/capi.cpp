@@ -109,9 +109,14 @@ long long usf_corr_fwd_workspace(int B, int C, int H, int W, int d) {
   return corr_fwd_workspace(B, C, H, W, d);
 }
 
+long long usf_corr_act_mask_words(int B, int H, int W, int d) {
+  if (B <= 0 || H <= 0 || W <= 0) return 0;
+  return corr_act_mask_words(B, H, W, d);
+}
+
 int usf_corr_fwd_ex_f32(const float* x1, const float* x2, float* out, long long out_bstride,
-                        int act, float slope, float* workspace, long long workspace_floats, int B,
-                        int C, int H, int W, int d, void* stream) {
+                        int act, float slope, unsigned long long* act_mask, float* workspace,
+                        long long workspace_floats, int B, int C, int H, int W, int d, void* stream) {
   clear_error();
   if (!check_dims("usf_corr_fwd_ex_f32", B, C, H, W)) return USF_EINVAL;
   if (d < 1 || d > 4) {
@@ -131,10 +136,16 @@ int usf_corr_fwd_ex_f32(const float* x1, const float* x2, float* out, long long 
     set_error("usf_corr_fwd_ex_f32: unknown act %d", act);
     return USF_EINVAL;
   }
+  if (act_mask && (act != USF_ACT_LEAKY_RELU || corr_act_mask_words(B, H, W, d) == 0)) {
+    set_error("usf_corr_fwd_ex_f32: act_mask needs act = LeakyReLU and W %% 4 == 0 (W=%d)", W);
+    return USF_EINVAL;
+  }
   if (const int pe = pre_check("usf_corr_fwd_ex_f32", (hipStream_t)stream)) return pe;
+  FwdEpi ep{out_bstride, act, slope};
+  ep.mask = act_mask;
   return finish("usf_corr_fwd_ex_f32",
-                corr_fwd_launch(x1, x2, out, B, C, H, W, d, (hipStream_t)stream,
-                                FwdEpi{out_bstride, act, slope}, workspace, workspace_floats),
+                corr_fwd_launch(x1, x2, out, B, C, H, W, d, (hipStream_t)stream, ep, workspace,
+                                workspace_floats),
                 (hipStream_t)stream);
 }
 
@@ -159,8 +170,9 @@ int usf_corr_bwd_f32(const float* x1, const float* x2, const float* gout, float*
 }
 
 int usf_corr_bwd_ex_f32(const float* x1, const float* x2, const float* gout, long long g_bstride,
-                        const float* act_out, float slope, float* scratch, float* gx1, float* gx2,
-                        int B, int C, int H, int W, int d, void* stream) {
+                        const float* act_out, const unsigned long long* act_mask, float slope,
+                        float* scratch, float* gx1, float* gx2, int B, int C, int H, int W, int d,
+                        void* stream) {
   clear_error();
   if (!check_dims("usf_corr_bwd_ex_f32", B, C, H, W)) return USF_EINVAL;
   if (d < 1 || d > 4) {
@@ -175,6 +187,19 @@ int usf_corr_bwd_ex_f32(const float* x1, const float* x2, const float* gout, lon
   if (g_bstride < k2 * H * W && B > 1) {
     set_error("usf_corr_bwd_ex_f32: gradient batch stride %lld < (2d+1)^2*H*W", g_bstride);
     return USF_EINVAL;
+  }
+  if (act_mask) {  // derivative from the forward's sign mask, inside the backward's g loads
+    if (corr_act_mask_words(B, H, W, d) == 0) {
+      set_error("usf_corr_bwd_ex_f32: act_mask needs W %% 4 == 0 (W=%d)", W);
+      return USF_EINVAL;
+    }
+    if (const int pe = pre_check("usf_corr_bwd_ex_f32", (hipStream_t)stream)) return pe;
+    BwdEpi ep{g_bstride};
+    ep.mask = act_mask;
+    ep.slope = slope;
+    return finish("usf_corr_bwd_ex_f32",
+                  corr_bwd_launch(x1, x2, gout, gx1, gx2, B, C, H, W, d, (hipStream_t)stream, ep),
+                  (hipStream_t)stream);
   }
   const bool fused = act_out && corr_bwd_fuses_act(d, W);
   if (act_out && !fused && !scratch) {

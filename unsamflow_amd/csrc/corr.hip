@@ -426,6 +426,47 @@ __global__ __launch_bounds__(64 * NDY) void corr_fwd_kernel(const float* __restr
         if (xb + i < W) o[i] = epi(acc[dx][i]);
     }
   }
+  if (leaky && ep.mask && (W & 3) == 0 && xb < W) {
+    // sign bits of this lane's activated outputs, one word per 4-pixel quad
+    // (the same test as the epilogue's: v = acc / C > 0)
+    unsigned long long* mw = ep.mask + ((size_t)(b * K + dy) * H + y) * (W >> 2) + (xb >> 2);
+#pragma unroll
+    for (int j = 0; j < PX / 4; ++j) {
+      unsigned long long bits = 0;
+#pragma unroll
+      for (int dx = 0; dx < K; ++dx)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          bits |= (unsigned long long)(acc[dx][4 * j + i] / cf > 0.f) << (4 * dx + i);
+      mw[j] = bits;
+    }
+  }
+}
+
+// The sign mask of FwdEpi::mask from the activated output itself, for the
+// channel-split forward (its reduce kernel applies the epilogue element-wise):
+// one thread per (b, dy, y, quad) reads the 9 dx planes' 4-pixel runs.
+template <int K>
+__global__ __launch_bounds__(256) void corr_act_mask_kernel(const float* __restrict__ out,
+                                                            long long obs,
+                                                            unsigned long long* __restrict__ mask,
+                                                            int B, int H, int W) {
+  const int W4 = W >> 2;
+  const long long n = (long long)B * K * H * W4;
+  const long long t = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (t >= n) return;
+  const int qd = (int)(t % W4);
+  const long long row = t / W4;  // (b * K + dy) * H + y
+  const int y = (int)(row % H);
+  const int dy = (int)((row / H) % K);
+  const int b = (int)(row / ((long long)H * K));
+  const float* o = out + (size_t)b * obs + (size_t)dy * K * H * W + (size_t)y * W + 4 * qd;
+  unsigned long long bits = 0;
+#pragma unroll
+  for (int dx = 0; dx < K; ++dx)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) bits |= (unsigned long long)(o[(size_t)dx * H * W + i] > 0.f) << (4 * dx + i);
+  mask[t] = bits;
 }
 
 // out[b * obs + k * HW + p] = epilogue(sum_g part[g][b][k][p] / C), g in order
@@ -474,6 +515,13 @@ hipError_t launch_fwd_v(const float* x1, const float* x2, float* out, int B, int
     const long long per = (long long)B * KHW;
     hipLaunchKernelGGL(corr_fwd_reduce_kernel, dim3((unsigned)((per + 1023) / 1024)), dim3(256), 0, s,
                        ep.part, out, ep, ep.groups, B, KHW, C);
+    if (ep.act && ep.mask) {
+      const hipError_t e2 = hipGetLastError();
+      if (e2 != hipSuccess) return e2;
+      const long long n = (long long)B * F::K * H * (W / 4);
+      hipLaunchKernelGGL(corr_act_mask_kernel<F::K>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
+                         out, ep.out_bstride, ep.mask, B, H, W);
+    }
   }
   return hipGetLastError();
 }
@@ -584,7 +632,13 @@ struct BwdCfg {
 
 // One (tile, channel group) of gx1 (G2 == false: from g and x2) or gx2
 // (G2 == true: from g and x1; mirrored indices).
-template <int D, int PX, int SEGX, int NW, int CC, int V, bool G2>
+__device__ __forceinline__ unsigned long long buf_load8(__amdgpu_buffer_rsrc_t r, int byte_off) {
+  using u32x2 = unsigned int __attribute__((ext_vector_type(2)));
+  const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(r, byte_off, 0, 0);
+  return (unsigned long long)v.x | ((unsigned long long)v.y << 32);
+}
+
+template <int D, int PX, int SEGX, int NW, int CC, int V, bool G2, bool AM>
 __device__ __forceinline__ void corr_bwd_tile(float* sm, const float* __restrict__ xs,
                                               const float* __restrict__ g,
                                               float* __restrict__ gx, int tile, int group, int b,
@@ -616,6 +670,12 @@ __device__ __forceinline__ void corr_bwd_tile(float* sm, const float* __restrict
   // raw buffer descriptors over this sample's K*K planes: 16-byte loads with a
   // 32-bit offset (one VGPR per address instead of a 64-bit pointer pair)
   const auto grs = plane_buf(gb, K * K * HW * 4);
+  // AM: the forward's LeakyReLU sign mask of sample b ([dy][y][x/4] words)
+  const int W4 = W >> 2;
+  const auto mrs = AM ? __builtin_amdgcn_make_buffer_rsrc(
+                            const_cast<unsigned long long*>(ep.mask + (size_t)b * K * H * W4), 0,
+                            K * H * W4 * 8, kRsrcFlags)
+                      : grs;
 
   // this wave's DYW rows of g for its PX pixels, read once. All loads are
   // unconditional at clamped in-bounds offsets (no branch, so no wait, inside
@@ -626,9 +686,24 @@ __device__ __forceinline__ void corr_bwd_tile(float* sm, const float* __restrict
   // load is clamped into the row and the lanes at the image edge pick their
   // elements out of it by index.
   float gv[DYW][K][PX];
+  static_assert(!AM || (PX == 4 && V == 4 && K <= 16), "sign-mask derivative: 4-pixel runs, W % 4 == 0");
 #pragma unroll
   for (int t = 0; t < DYW; ++t) {
     const int dy = wave * DYW + t;
+    // AM: sign words of this row -- gx1: the lane's own quad; gx2: its runs
+    // start at xb - dx + d, so the quads left of, at and right of xb
+    unsigned long long mw[3] = {0, 0, 0};
+    if constexpr (AM) {
+      const int yy = G2 ? y - dy + D : y;
+      const bool rowok = dy < K && (unsigned)yy < (unsigned)H;
+      const int mrow = (min(dy, K - 1) * H + (rowok ? yy : 0)) * W4;
+      const int q0 = xb >> 2;
+#pragma unroll
+      for (int o = G2 ? -1 : 0; o <= (G2 ? 1 : 0); ++o) {
+        const int qq = min(max(q0 + o, 0), W4 - 1);
+        mw[o + 1] = buf_load8(mrs, (mrow + qq) * 8);
+      }
+    }
 #pragma unroll
     for (int dx = 0; dx < K; ++dx) {
       const int k = min(dy, K - 1) * K + dx;
@@ -648,7 +723,15 @@ __device__ __forceinline__ void corr_bwd_tile(float* sm, const float* __restrict
             const bool ok = rowok && (unsigned)xx < (unsigned)W;
             // gx2's edge lanes pick their element by index; gx1 runs are aligned, never shifted
             const int idx = G2 ? i + shift : i;
-            const float e = idx <= 0 ? v.x : idx == 1 ? v.y : idx == 2 ? v.z : v.w;
+            float e = idx <= 0 ? v.x : idx == 1 ? v.y : idx == 2 ? v.z : v.w;
+            if constexpr (AM) {
+              // LeakyReLU derivative (on the result, as the in-place module):
+              // pixel xb + ei of the row, ei in [-d, 3 + d]; compile-time word and bit
+              const int ei = G2 ? i4 + i - dx + D : i4 + i;
+              const unsigned long long wd = mw[(ei + 4) >> 2];
+              const bool pos = (wd >> (4 * dx + (ei & 3))) & 1ull;
+              e = pos ? e : e * ep.slope;
+            }
             gv[t][dx][i4 + i] = ok ? e : 0.f;
           }
         }
@@ -758,7 +841,7 @@ __device__ __forceinline__ void corr_bwd_tile(float* sm, const float* __restrict
 #ifndef USF_BWD_WAVES_PER_EU
 #define USF_BWD_WAVES_PER_EU 3
 #endif
-template <int D, int PX, int SEGX, int NW, int CC, int V, int MODE>
+template <int D, int PX, int SEGX, int NW, int CC, int V, int MODE, bool AM>
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(USF_BWD_WAVES_PER_EU))) void corr_bwd_kernel(const float* __restrict__ x1,
                                                            const float* __restrict__ x2,
                                                            const float* __restrict__ g,
@@ -793,16 +876,16 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(USF_BWD
   const int tile = (w / gridDim.y) % gridDim.x;
   int b = w / (gridDim.x * gridDim.y);
   if constexpr (MODE == 1) {
-    corr_bwd_tile<D, PX, SEGX, NW, CC, V, false>(sm, x2, g, gx1, tile, group, b, C, H, W, tiles_x, cg, ep);
+    corr_bwd_tile<D, PX, SEGX, NW, CC, V, false, AM>(sm, x2, g, gx1, tile, group, b, C, H, W, tiles_x, cg, ep);
   } else if constexpr (MODE == 2) {
-    corr_bwd_tile<D, PX, SEGX, NW, CC, V, true>(sm, x1, g, gx2, tile, group, b, C, H, W, tiles_x, cg, ep);
+    corr_bwd_tile<D, PX, SEGX, NW, CC, V, true, AM>(sm, x1, g, gx2, tile, group, b, C, H, W, tiles_x, cg, ep);
   } else {
     if (b >= B)
-      corr_bwd_tile<D, PX, SEGX, NW, CC, V, true>(sm, x1, g, gx2, tile, group, b - B, C, H, W,
-                                                  tiles_x, cg, ep);
+      corr_bwd_tile<D, PX, SEGX, NW, CC, V, true, AM>(sm, x1, g, gx2, tile, group, b - B, C, H, W,
+                                                      tiles_x, cg, ep);
     else
-      corr_bwd_tile<D, PX, SEGX, NW, CC, V, false>(sm, x2, g, gx1, tile, group, b, C, H, W,
-                                                   tiles_x, cg, ep);
+      corr_bwd_tile<D, PX, SEGX, NW, CC, V, false, AM>(sm, x2, g, gx1, tile, group, b, C, H, W,
+                                                       tiles_x, cg, ep);
   }
 }
 
@@ -823,7 +906,15 @@ hipError_t launch_bwd_mode(const float* x1, const float* x2, const float* g, flo
   groups = max(1, min(groups, (C + CC - 1) / CC));
   const int cg = round_up((C + groups - 1) / groups, CC);
   dim3 grid(tiles_x * tiles_y, (C + cg - 1) / cg, B * dirs);
-  hipLaunchKernelGGL((corr_bwd_kernel<D, PX, SEGX, NW, CC, V, MODE>), grid, dim3(F::NT), 0, s, x1,
+  if constexpr (V == 4 && PX == 4) {
+    if (ep.mask) {
+      hipLaunchKernelGGL((corr_bwd_kernel<D, PX, SEGX, NW, CC, V, MODE, true>), grid, dim3(F::NT), 0, s,
+                         x1, x2, g, gx1, gx2, B, C, H, W, tiles_x, cg, ep);
+      return hipGetLastError();
+    }
+  }
+  if (ep.mask) return hipErrorInvalidValue;  // the sign mask needs W % 4 == 0 (capi checks)
+  hipLaunchKernelGGL((corr_bwd_kernel<D, PX, SEGX, NW, CC, V, MODE, false>), grid, dim3(F::NT), 0, s, x1,
                      x2, g, gx1, gx2, B, C, H, W, tiles_x, cg, ep);
   return hipGetLastError();
 }
@@ -949,6 +1040,11 @@ long long corr_fwd_workspace(int B, int C, int H, int W, int d) {
 // offsets, or only its signs packed into bits) spilled 250-600 bytes past the
 // 168-VGPR budget of the 3-waves/SIMD backward in every arrangement tried.
 bool corr_bwd_fuses_act(int, int) { return false; }
+
+long long corr_act_mask_words(int B, int H, int W, int d) {
+  if (W % 4 != 0 || d < 1 || d > 4) return 0;
+  return (long long)B * (2 * d + 1) * H * (W / 4);
+}
 
 hipError_t corr_bwd_launch(const float* x1, const float* x2, const float* gout, float* gx1,
                            float* gx2, int B, int C, int H, int W, int d, hipStream_t s, BwdEpi ep) {

@@ -66,10 +66,18 @@ struct FwdEpi {
   // kernel applies the mean and the epilogue. Not part of the C ABI.
   float* part = nullptr;
   int groups = 1;
+  // LeakyReLU sign mask (act != 0, W % 4 == 0): word [b][dy][y][x / 4] holds
+  // bit 4 dx + (x % 4) = (activated output at (dy, dx, y, x) > 0). The backward
+  // applies the derivative from it instead of re-reading the activated output.
+  unsigned long long* mask = nullptr;
 };
 struct BwdEpi {
   long long g_bstride;
+  const unsigned long long* mask = nullptr;  // FwdEpi::mask of the forward: derivative in the prologue
+  float slope = 0.f;
 };
+// words of the sign mask (0: layout unsupported, W % 4 != 0)
+long long corr_act_mask_words(int B, int H, int W, int d);
 hipError_t leaky_bwd_gather_launch(const float* g, const float* act, long long g_bstride,
                                    float slope, float* out, int B, int K2, int H, int W,
                                    hipStream_t s);

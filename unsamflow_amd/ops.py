@@ -69,7 +69,7 @@ def corr_forward(x1: torch.Tensor, x2: torch.Tensor, max_displacement: int,
         # the _ex entry with a dense output stride: same result as usf_corr_fwd_f32,
         # plus the channel-split workspace for the small levels
         rc = lib.usf_corr_fwd_ex_f32(
-            x1c.data_ptr(), x2c.data_ptr(), out.data_ptr(), K * K * H * W, 0, 0.0,
+            x1c.data_ptr(), x2c.data_ptr(), out.data_ptr(), K * K * H * W, 0, 0.0, None,
             ws.data_ptr() if nws else None, nws, B, C, H, W, d, _lib.stream_handle(x1.device)
         )
     _lib.check(rc, "usf_corr_fwd_ex_f32")
@@ -352,11 +352,22 @@ def _plane_slice_stride(name: str, t: torch.Tensor, shape) -> int:
     return s[0] if B > 1 else K * H * W
 
 
+def corr_act_mask(B: int, H: int, W: int, max_displacement: int, device) -> torch.Tensor | None:
+    """An empty LeakyReLU sign mask for :func:`corr_forward_ex` (int64 words,
+    [B,2d+1,H,W/4]), or None where the layout needs W % 4 == 0 and W is not."""
+    n = int(_lib.load().usf_corr_act_mask_words(B, H, W, int(max_displacement)))
+    if n == 0:
+        return None
+    return torch.empty((B, 2 * int(max_displacement) + 1, H, W // 4), device=device, dtype=torch.int64)
+
+
 def corr_forward_ex(x1: torch.Tensor, x2: torch.Tensor, max_displacement: int, out: torch.Tensor,
-                    leaky_slope: float | None = None) -> torch.Tensor:
+                    leaky_slope: float | None = None, act_mask: torch.Tensor | None = None) -> torch.Tensor:
     """:func:`corr_forward` into ``out``, a [B,(2d+1)^2,H,W] channel slice of a
     larger NCHW buffer (the flow estimator's concat input), with the decoder's
-    LeakyReLU applied in the kernel epilogue when ``leaky_slope`` is given."""
+    LeakyReLU applied in the kernel epilogue when ``leaky_slope`` is given; with
+    ``act_mask`` (:func:`corr_act_mask`) the epilogue also writes the output's
+    sign bits for :func:`corr_backward_ex`."""
     _require_device_f32("input1", x1)
     _require_device_f32("input2", x2)
     _require_device_f32("output", out)
@@ -369,12 +380,16 @@ def corr_forward_ex(x1: torch.Tensor, x2: torch.Tensor, max_displacement: int, o
     x1c, x2c = x1.contiguous(), x2.contiguous()
     lib = _lib.load()
     act = 0 if leaky_slope is None else 1
+    if act_mask is not None:
+        if act == 0 or act_mask.dtype != torch.int64 or not act_mask.is_contiguous() \
+                or act_mask.numel() != int(lib.usf_corr_act_mask_words(B, H, W, d)):
+            raise ValueError("act_mask: a contiguous int64 corr_act_mask() tensor with leaky_slope set")
     ws, nws = _corr_workspace(lib, B, C, H, W, d, x1.device)
     with torch.cuda.device(x1.device), _kt.timed(
         "corr_fwd", (B, C, H, W), x1.device, _kt.corr_bytes(B, C, H, W, K * K), _kt.corr_flops(B, C, H, W, K * K)
     ):
         rc = lib.usf_corr_fwd_ex_f32(x1c.data_ptr(), x2c.data_ptr(), out.data_ptr(), obs, act,
-                                     float(leaky_slope or 0.0), ws.data_ptr() if nws else None, nws,
+                                     float(leaky_slope or 0.0), _ptr(act_mask), ws.data_ptr() if nws else None, nws,
                                      B, C, H, W, d, _lib.stream_handle(x1.device))
     _lib.check(rc, "usf_corr_fwd_ex_f32")
     return out
@@ -382,10 +397,13 @@ def corr_forward_ex(x1: torch.Tensor, x2: torch.Tensor, max_displacement: int, o
 
 def corr_backward_ex(x1: torch.Tensor, x2: torch.Tensor, grad_out: torch.Tensor, max_displacement: int,
                      need_x1: bool = True, need_x2: bool = True, act_out: torch.Tensor | None = None,
-                     leaky_slope: float = 0.1) -> tuple[torch.Tensor | None, torch.Tensor | None]:
+                     leaky_slope: float = 0.1, act_mask: torch.Tensor | None = None,
+                     ) -> tuple[torch.Tensor | None, torch.Tensor | None]:
     """:func:`corr_backward` reading ``grad_out`` as a channel slice of the concat
     gradient; with ``act_out`` (the forward's activated slice) the LeakyReLU
-    derivative is applied first (one dense pass into a scratch)."""
+    derivative is applied first (one dense pass into a scratch); with
+    ``act_mask`` (the forward's sign mask) it is applied inside the backward
+    kernel's gradient loads instead, and ``act_out`` is not read."""
     _require_device_f32("input1", x1)
     _require_device_f32("input2", x2)
     _require_device_f32("grad_output", grad_out)
@@ -395,7 +413,12 @@ def corr_backward_ex(x1: torch.Tensor, x2: torch.Tensor, grad_out: torch.Tensor,
     gbs = _plane_slice_stride("grad_output", grad_out, (B, K * K, H, W))
     scratch = None
     lib = _lib.load()
-    if act_out is not None:
+    if act_mask is not None:
+        if act_mask.dtype != torch.int64 or not act_mask.is_contiguous() \
+                or act_mask.numel() != int(lib.usf_corr_act_mask_words(B, H, W, d)):
+            raise ValueError("act_mask: the forward's contiguous int64 corr_act_mask() tensor")
+        act_out = None
+    elif act_out is not None:
         _require_device_f32("act_out", act_out)
         if _plane_slice_stride("act_out", act_out, (B, K * K, H, W)) != gbs:
             raise ValueError("act_out and grad_output must share the batch stride")
@@ -409,16 +432,19 @@ def corr_backward_ex(x1: torch.Tensor, x2: torch.Tensor, grad_out: torch.Tensor,
     g2 = torch.empty_like(x2c) if need_x2 else None
     # with the LeakyReLU derivative the site also reads the activated output
     # once (what leaky_relu_backward needs): a distinct site, its bytes included
-    op = "corr_bwd" if act_out is None else "corr_bwd_leaky"
+    # (with the sign mask instead: its words are the derivative's input)
+    op = "corr_bwd" if act_out is None and act_mask is None else "corr_bwd_leaky"
     nbytes = _kt.corr_bytes(B, C, H, W, K * K, True, need_x1, need_x2)
     if act_out is not None:
         nbytes += 4 * B * H * W * K * K
+    elif act_mask is not None:
+        nbytes += 8 * act_mask.numel()
     with torch.cuda.device(x1.device), _kt.timed(
         op, (B, C, H, W, need_x1, need_x2), x1.device, nbytes,
         _kt.corr_flops(B, C, H, W, K * K, True, need_x1, need_x2),
     ):
         rc = lib.usf_corr_bwd_ex_f32(x1c.data_ptr(), x2c.data_ptr(), grad_out.data_ptr(), gbs, _ptr(act_out),
-                                     float(leaky_slope), _ptr(scratch), _ptr(g1), _ptr(g2), B, C, H, W, d,
+                                     _ptr(act_mask), float(leaky_slope), _ptr(scratch), _ptr(g1), _ptr(g2), B, C, H, W, d,
                                      _lib.stream_handle(x1.device))
     _lib.check(rc, "usf_corr_bwd_ex_f32")
     return g1, g2
