@@ -854,11 +854,11 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(USF_BWD
   USF_TRACE_HWID();
   // work item: channel group fastest (the groups of a tile share its g planes),
   // then tile, then (direction, sample); grid = (tiles, groups, B * dirs).
-  // No XCD remap here. Measured twice on the box (tools/ab_build.py): remapping
-  // this order (L4 85 vs 59 us) and a direction-fastest order dealt to the XCDs
-  // in contiguous chunks, so a tile's gx1/gx2 and its neighbours share one L2
-  // (L4 84 vs 59 us, L3 51 vs 43 us) are both slower, although they cut the
-  // FETCH traffic (2.6x -> 1.4x of algorithmic).
+  // Whole-sample XCD orders were measured slower on the box (tools/ab_build.py):
+  // remapping this order (L4 85 vs 59 us) and a direction-fastest order dealt
+  // to the XCDs in contiguous chunks (L4 84 vs 59 us, L3 51 vs 43 us), although
+  // they cut the FETCH traffic (2.6x -> 1.4x of algorithmic). Short chunks
+  // (below) keep both.
 #ifndef USF_BWD_CHUNK
 #define USF_BWD_CHUNK 14
 #endif
@@ -1035,10 +1035,11 @@ long long corr_fwd_workspace(int B, int C, int H, int W, int d) {
   return (long long)p.groups * B * K * K * H * W;
 }
 
-// The LeakyReLU derivative is a separate dense pass (leaky_bwd_gather_kernel).
-// Fusing it into the g loads (the forward's activated output loaded at the same
-// offsets, or only its signs packed into bits) spilled 250-600 bytes past the
-// 168-VGPR budget of the 3-waves/SIMD backward in every arrangement tried.
+// With act_out (no sign mask) the LeakyReLU derivative is a separate dense pass
+// (leaky_bwd_gather_kernel): loading the activated output itself next to g in
+// the prologue spilled 250-600 bytes past the 168-VGPR budget of the
+// 3-waves/SIMD backward. The forward's sign mask (BwdEpi::mask, 6-18 extra
+// VGPRs) is the fused form.
 bool corr_bwd_fuses_act(int, int) { return false; }
 
 long long corr_act_mask_words(int B, int H, int W, int d) {
