@@ -149,8 +149,9 @@ int usf_warp_fwd_f32(const float* x, const float* flow, long long flow_bstride,
                      void* stream);
 
 /* Backward of usf_warp_fwd_f32. gout: [B,C,H,W] dense.
- * gx: [B,C,H,W] or NULL; it is ACCUMULATED into (fp32 atomics) and must be
- *     zeroed by the caller; summation order is not deterministic.
+ * gx: [B,C,H,W] or NULL; overwritten (the library zeroes it, then scatters
+ *     with fp32 atomics: summation order not fixed). Variant 4 of
+ *     usf_set_variant(2, .) gathers instead for sources with |flow| < 2 px.
  * gflow: [B,2,H,W] dense or NULL; overwritten, deterministic. */
 int usf_warp_bwd_f32(const float* x, const float* flow, long long flow_bstride,
                      const float* gout, float* gx, float* gflow,
@@ -261,7 +262,8 @@ int usf_area_pyramid_f32(const float* x, float* out1, float* out2, float* out3, 
  * op 0 = correlation forward tile config, op 1 = correlation backward tile
  * config, op 2 = warp grad_x scatter (0 = wave reduce-by-key + direct global
  * atomics, 1 = LDS-aggregated tiles, 2 / 3 = variant 0 with 4 / 1 channel
- * slices per workgroup); index -1 restores the built-in choice. Returns the number of
+ * slices per workgroup, 4 = gather for |flow| < 2 px + scatter for the rest);
+ * index -1 restores the built-in choice. Returns the number of
  * variants of `op` (so index range is [0, n)), or USF_EINVAL for an unknown op
  * or out-of-range index. Process-wide; set it before launching, not
  * concurrently with launches. */

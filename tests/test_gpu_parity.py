@@ -338,17 +338,19 @@ def test_corr_every_tile_variant_vs_oracle(hip_device, shape):
         lib.usf_set_variant(1, -1)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
 def test_warp_grad_x_scatter_variants(hip_device, variant):
-    """Every grad_x scatter variant (reduce-by-key atomics with any channel split,
-    LDS-aggregated tiles) matches the oracle,
-    including a large-flow case whose target boxes overflow the LDS budget."""
+    """Every grad_x variant (reduce-by-key atomics with any channel split,
+    LDS-aggregated tiles, the gather with its outlier scatter) matches the
+    oracle, including a large-flow case whose target boxes overflow the LDS
+    budget (and whose sources are mostly gather outliers)."""
     from unsamflow_amd import _lib, ops
 
     lib = _lib.load()
     try:
         lib.usf_set_variant(2, variant)
-        for shape, scale, seed in [((2, 32, 24, 40), 2.0, 1), ((1, 64, 16, 52), 25.0, 2), ((2, 3, 33, 17), 6.0, 3)]:
+        for shape, scale, seed in [((2, 32, 24, 40), 2.0, 1), ((1, 64, 16, 52), 25.0, 2), ((2, 3, 33, 17), 6.0, 3),
+                                   ((2, 20, 9, 70), 1.0, 4)]:
             x = hashrng.uniform(shape, 300 + seed)
             flow = hashrng.symmetric((shape[0], 2) + shape[2:], 400 + seed, scale)
             g = hashrng.normal(shape, 500 + seed)

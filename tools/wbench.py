@@ -38,7 +38,7 @@ def main():
     lib = _lib.load()
     dev = torch.device("cuda:0")
     res = []
-    for (B, C, H, W) in [(8, 32, 64, 208), (8, 64, 32, 104), (8, 96, 16, 52), (8, 128, 8, 26)]:
+    for (B, C, H, W) in [(16, 32, 64, 208), (16, 64, 32, 104), (16, 96, 16, 52), (16, 128, 8, 26)]:
         g = torch.Generator(device=dev).manual_seed(1)
         x = torch.rand(B, C, H, W, device=dev, generator=g)
         go = torch.randn(B, C, H, W, device=dev, generator=g)
@@ -47,7 +47,8 @@ def main():
         print(f"{(B, C, H, W)} memset grad_x {z:.2f} us", flush=True)
         for fname, fl in flows(B, H, W, dev).items():
             for need_x, need_f in ((True, True), (True, False), (False, True)):
-                for v in ((-1, 1, 2, 3) if need_x else (-1,)):
+                # -1: lane-merged scatter (default); 1: LDS-aggregated scatter; 4: gather grad_x
+                for v in ((-1, 1, 4) if need_x else (-1,)):
                     lib.usf_set_variant(2, v)
                     t = device_time_us(lambda: ops.warp_backward(x, fl, go, "border", need_x, need_f))
                     row = {"shape": [B, C, H, W], "flow": fname, "grad_x": need_x, "grad_flow": need_f,

@@ -147,7 +147,15 @@ __device__ __forceinline__ void scatter_row(float* gc, int o_w, int o_e, bool m_
   }
 }
 
-template <bool BORDER, bool WANT_GX, bool WANT_GF, int CS>
+// grad_x gather (warp_gx_gather_kernel) covers source pixels whose flow is
+// below kGatherR pixels in both components ("inliers"); the scatter below,
+// with OUTL, adds the rest.
+constexpr int kGatherR = 2;
+__device__ __forceinline__ bool gather_inlier(float u, float v) {
+  return fabsf(u) < (float)kGatherR && fabsf(v) < (float)kGatherR;  // false for NaN
+}
+
+template <bool BORDER, bool WANT_GX, bool WANT_GF, int CS, bool OUTL = false>
 __global__ __launch_bounds__(256) void warp_bwd_kernel(const float* __restrict__ x,
                                                        const float* __restrict__ flow,
                                                        long long fbs,
@@ -164,16 +172,18 @@ __global__ __launch_bounds__(256) void warp_bwd_kernel(const float* __restrict__
   int bx, b;
   warp_block(bx, b);
   const int p = bx * PXB + pl;
-  const bool valid = p < HW;
+  bool valid = p < HW;
   float dix = 0.f, diy = 0.f;
   Tap tp{};
   if (valid) {
     const int y = p / W, xx = p - y * W;
     const float* fb = flow + b * fbs;
-    tp = make_tap(fb[p], fb[HW + p], xx, y, H, W, BORDER);
-  } else {
-    tp.m_nw = tp.m_ne = tp.m_sw = tp.m_se = false;
+    const float u = fb[p], v = fb[HW + p];
+    if (OUTL) valid = !gather_inlier(u, v);  // the gather kernel has the inliers
+    tp = make_tap(u, v, xx, y, H, W, BORDER);
   }
+  if (!valid) tp.m_nw = tp.m_ne = tp.m_sw = tp.m_se = false;
+  if (OUTL && !__syncthreads_or(valid)) return;  // no outlier in this workgroup (uniform)
   // grad_x: reduce-by-key over the wave per corner row (see scatter_row)
   RowRuns rn{}, rs{};
   if (WANT_GX) {
@@ -233,6 +243,89 @@ __global__ __launch_bounds__(256) void warp_bwd_kernel(const float* __restrict__
     gf[0] = (ggx / (float)(W - 1)) * 2.0f;
     gf[HW] = (ggy / (float)(H - 1)) * 2.0f;
   }
+}
+
+// grad_x as a gather (no atomics for inliers, no zero fill; usf_set_variant(2, 4)). A workgroup
+// owns a GTW x GTH tile of target cells and GCC channels. Phase 1: the taps of
+// every source pixel within kGatherR + 1 of the tile (make_tap, the same
+// coordinate chain as the scatter) go to LDS -- the north-west corner packed
+// relative to the tile and the four corner weights, zeroed where a corner is
+// off-image; sources that are not inliers get no corner. Phase 2: each thread
+// (one target cell q) scans the (2R+3)^2 sources that can reach q, in a fixed
+// order; a source whose corner is q adds weight * gout[c][source] for the
+// workgroup's channels. Sources with |flow| >= R are added afterwards by the
+// scatter (warp_bwd_kernel<..., OUTL>).
+constexpr int GTW = 32, GTH = 8, GCC = 16;
+constexpr int GWX = GTW + 2 * kGatherR + 2, GWY = GTH + 2 * kGatherR + 2;  // source window
+constexpr int GWN = GWX * GWY;
+
+template <bool BORDER>
+__global__ __launch_bounds__(256) void warp_gx_gather_kernel(const float* __restrict__ flow, long long fbs,
+                                                             const float* __restrict__ gout,
+                                                             float* __restrict__ gx, int C, int H, int W,
+                                                             int tiles_x, int chunks) {
+  constexpr int R = kGatherR;
+  __shared__ int spos[GWN];        // (yn - wy0) << 16 | (xw - wx0), or -1: no corner
+  __shared__ float swt[4][GWN];    // nw, ne, sw, se weights (0 where masked)
+  const int HW = H * W;
+  const int t = threadIdx.x;
+  const int tile = blockIdx.x;
+  const int b = blockIdx.y / chunks, chunk = blockIdx.y - b * chunks;
+  const int ty = tile / tiles_x, tx = tile - ty * tiles_x;
+  const int x0 = tx * GTW, y0 = ty * GTH;
+  const int wx0 = x0 - R - 1, wy0 = y0 - R - 1;  // window origin (source coordinates)
+  const float* fb = flow + b * fbs;
+  for (int i = t; i < GWN; i += 256) {
+    const int sy = wy0 + i / GWX, sx = wx0 + i % GWX;
+    int pos = -1;
+    float w4[4] = {0.f, 0.f, 0.f, 0.f};
+    if ((unsigned)sy < (unsigned)H && (unsigned)sx < (unsigned)W) {
+      const int s = sy * W + sx;
+      const float u = fb[s], v = fb[HW + s];
+      if (gather_inlier(u, v)) {
+        const Tap tp = make_tap(u, v, sx, sy, H, W, BORDER);
+        // inliers land within R + 1 of the source: relative corner in [0, GWX)
+        pos = ((tp.yn - wy0) << 16) | (tp.xw - wx0);
+        w4[0] = tp.m_nw ? tp.s * tp.e : 0.f;
+        w4[1] = tp.m_ne ? tp.s * tp.w : 0.f;
+        w4[2] = tp.m_sw ? tp.n * tp.e : 0.f;
+        w4[3] = tp.m_se ? tp.n * tp.w : 0.f;
+      }
+    }
+    spos[i] = pos;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) swt[k][i] = w4[k];
+  }
+  __syncthreads();
+  const int qx = x0 + (t % GTW), qy = y0 + (t / GTW);
+  if (qx >= W || qy >= H) return;
+  const int c0 = chunk * GCC;
+  const int nc = min(GCC, C - c0);
+  const float* gb = gout + ((size_t)b * C + c0) * HW;
+  float acc[GCC];
+#pragma unroll
+  for (int c = 0; c < GCC; ++c) acc[c] = 0.f;
+  // q relative to the window; sources within R + 1 of q in both axes
+  const int rx = qx - wx0, ry = qy - wy0;
+  for (int dy = -R - 1; dy <= R + 1; ++dy) {
+    for (int dx = -R - 1; dx <= R + 1; ++dx) {
+      const int i = (ry + dy) * GWX + (rx + dx);
+      const int pos = spos[i];
+      if (pos < 0) continue;
+      const int cx = rx - (pos & 0xFFFF), cy = ry - (pos >> 16);  // q - north-west corner
+      if ((unsigned)cx > 1u || (unsigned)cy > 1u) continue;
+      const float w = swt[cy * 2 + cx][i];
+      if (w == 0.f) continue;
+      const int s = (wy0 + ry + dy) * W + (wx0 + rx + dx);
+#pragma unroll
+      for (int c = 0; c < GCC; ++c)
+        if (c < nc) acc[c] = fmaf(w, gb[(size_t)c * HW + s], acc[c]);
+    }
+  }
+  float* gq = gx + ((size_t)b * C + c0) * HW + qy * W + qx;
+#pragma unroll
+  for (int c = 0; c < GCC; ++c)
+    if (c < nc) gq[(size_t)c * HW] = acc[c];
 }
 
 // grad_x with the corner scatter pre-summed in LDS. A workgroup owns a 2-D
@@ -451,12 +544,48 @@ void bwd_launch_cs(const float* x, const float* flow, long long fbs, const float
                        fbs, gout, gx, gflow, B, C, H, W);
 }
 
+// grad_x by gather (+ the scatter for |flow| >= kGatherR), grad_flow by the
+// scatter kernel's channel reduction without its grad_x part.
+template <bool BORDER, int CS>
+void bwd_gather_cs(const float* x, const float* flow, long long fbs, const float* gout, float* gx,
+                   float* gflow, int B, int C, int H, int W, hipStream_t s) {
+  const dim3 grid((unsigned)((H * W + 256 / CS - 1) / (256 / CS)), (unsigned)B), block(256);
+  if (gflow)
+    hipLaunchKernelGGL((warp_bwd_kernel<BORDER, false, true, CS>), grid, block, 0, s, x, flow, fbs, gout,
+                       nullptr, gflow, B, C, H, W);
+  const int tiles_x = (W + GTW - 1) / GTW, tiles_y = (H + GTH - 1) / GTH;
+  const int chunks = (C + GCC - 1) / GCC;
+  hipLaunchKernelGGL((warp_gx_gather_kernel<BORDER>), dim3((unsigned)(tiles_x * tiles_y), (unsigned)(B * chunks)),
+                     block, 0, s, flow, fbs, gout, gx, C, H, W, tiles_x, chunks);
+  hipLaunchKernelGGL((warp_bwd_kernel<BORDER, true, false, CS, true>), grid, block, 0, s, x, flow, fbs, gout,
+                     gx, nullptr, B, C, H, W);
+}
+
 template <bool BORDER>
 void bwd_launch_pad(const float* x, const float* flow, long long fbs, const float* gout,
                     float* gx, float* gflow, int B, int C, int H, int W, hipStream_t s) {
   // usf_set_variant(2, 2 / 3): lane-merged scatter with CS forced to 4 / 1
   // (whole-wave pixel runs) instead of the occupancy-driven choice
   const int v = variant_override(2);
+  // usf_set_variant(2, 4): deterministic gather for grad_x. Measured against the
+  // lane-merged scatter at the decoder's batch-16 shapes (profiles/ab_r01/
+  // warp_gather.json): faster for near-zero flows (L4 53 vs 81 us, L1 21 vs
+  // 28 us), slower for +-2 px fields at L2/L3 (60 vs 51, 98 vs 90 us) and for
+  // +-8 px fields everywhere (most sources are scatter outliers), so it is
+  // opt-in.
+  if (gx && v == 4) {
+    const long runs64g = (long)B * ((H * W + 63) / 64);
+    const int csg = (runs64g >= 96 && C >= 4) ? 4 : pick_cs(B, C, H * W);
+    switch (csg) {
+      case 1: bwd_gather_cs<BORDER, 1>(x, flow, fbs, gout, gx, gflow, B, C, H, W, s); break;
+      case 4: bwd_gather_cs<BORDER, 4>(x, flow, fbs, gout, gx, gflow, B, C, H, W, s); break;
+      case 16: bwd_gather_cs<BORDER, 16>(x, flow, fbs, gout, gx, gflow, B, C, H, W, s); break;
+      default: bwd_gather_cs<BORDER, 64>(x, flow, fbs, gout, gx, gflow, B, C, H, W, s); break;
+    }
+    return;
+  }
+  // the scatter variants accumulate into gx: zero it first (gx is overwritten either way)
+  if (gx) (void)hipMemsetAsync(gx, 0, sizeof(float) * (size_t)B * C * H * W, s);
   // Default: CS = 4 (each wave one 64-pixel run of one channel, so an atomic
   // wave-instruction covers one contiguous row piece) whenever that still gives
   // ~100 workgroups; narrower pixel runs (CS 16/64) only for the tiny levels.

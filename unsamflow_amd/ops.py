@@ -189,7 +189,7 @@ def warp_backward(
     xc = x.contiguous()
     fv, fbs = _flow_view(flow, B, H, W)
     gc = grad_out.contiguous()
-    gx = torch.zeros_like(xc) if need_x else None
+    gx = torch.empty_like(xc) if need_x else None  # overwritten by the library
     gf = torch.empty((B, 2, H, W), device=x.device, dtype=torch.float32) if need_flow else None
     lib = _lib.load()
     with torch.cuda.device(x.device), _kt.timed(
