@@ -872,9 +872,24 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(USF_BWD
     // slower (84 us) and so are levels with < 16 tiles (L1 11.6 -> 13.5 us).
     w = xcd_chunk(w, gridDim.x * gridDim.y * gridDim.z, USF_BWD_CHUNK);
   }
-  const int group = w % gridDim.y;
-  const int tile = (w / gridDim.y) % gridDim.x;
-  int b = w / (gridDim.x * gridDim.y);
+#ifndef USF_BWD_DIRFAST
+#define USF_BWD_DIRFAST 0
+#endif
+  int group, tile, b;
+  if (MODE == 3 && USF_BWD_DIRFAST) {
+    // direction fastest: a tile's gx1 and gx2 items are neighbours in the
+    // chunk (same XCD, same time), so the second read of its g slice can hit L2.
+    // Measured at batch 16 (profiles/ab_r01/bwd_dirfast.json): no change
+    // (L4 74.4 vs 75.4 us; 72.6 with 28-item chunks), so off by default.
+    const int dir = w & 1, w2 = w >> 1;
+    group = w2 % gridDim.y;
+    tile = (w2 / gridDim.y) % gridDim.x;
+    b = w2 / (gridDim.x * gridDim.y) + (dir ? B : 0);
+  } else {
+    group = w % gridDim.y;
+    tile = (w / gridDim.y) % gridDim.x;
+    b = w / (gridDim.x * gridDim.y);
+  }
   if constexpr (MODE == 1) {
     corr_bwd_tile<D, PX, SEGX, NW, CC, V, false, AM>(sm, x2, g, gx1, tile, group, b, C, H, W, tiles_x, cg, ep);
   } else if constexpr (MODE == 2) {
