@@ -573,11 +573,19 @@ FwdPlan fwd_plan(int B, int C, int H, int W) {
   const long big = (long)B * ((W + 63) / 64) * ((H + 7) / 8);
   if (big >= 256) p.cfg = 0;
   else if ((long)B * tiles32 >= 256) p.cfg = 1;
+// split below 192 workgroups into ~384: at batch 16 splitting more (L2 into
+// 2-6 groups) is slower, 22-26 vs 18.4 us (profiles/ab_r01/fwd_split_b16.json)
+#ifndef USF_FWD_SPLIT_BELOW
+#define USF_FWD_SPLIT_BELOW 192
+#endif
+#ifndef USF_FWD_SPLIT_TARGET
+#define USF_FWD_SPLIT_TARGET 384
+#endif
   if (p.cfg == 2) {
     const long wgs = (long)B * tiles32 * ((K + 2) / 3);
-    if (wgs < 192) {
+    if (wgs < USF_FWD_SPLIT_BELOW) {
       const int CC = 8;
-      int g = (int)((384 + wgs - 1) / wgs);
+      int g = (int)((USF_FWD_SPLIT_TARGET + wgs - 1) / wgs);
       p.groups = std::max(1, std::min(g, C / (2 * CC)));
     }
   }
