@@ -201,14 +201,13 @@ int usf_corr_bwd_ex_f32(const float* x1, const float* x2, const float* gout, lon
                   corr_bwd_launch(x1, x2, gout, gx1, gx2, B, C, H, W, d, (hipStream_t)stream, ep),
                   (hipStream_t)stream);
   }
-  const bool fused = act_out && corr_bwd_fuses_act(d, W);
-  if (act_out && !fused && !scratch) {
+  if (act_out && !scratch) {
     set_error("usf_corr_bwd_ex_f32: act_out needs a scratch of usf_corr_bwd_ex_scratch() floats here");
     return USF_EINVAL;
   }
   if (const int pe = pre_check("usf_corr_bwd_ex_f32", (hipStream_t)stream)) return pe;
   const BwdEpi ep{g_bstride};
-  if (act_out && !fused) {  // derivative + de-concat in one dense pass, then the plain backward
+  if (act_out) {  // derivative + de-concat in one dense pass, then the plain backward
     const hipError_t e = leaky_bwd_gather_launch(gout, act_out, g_bstride, slope, scratch, B,
                                                  (int)k2, H, W, (hipStream_t)stream);
     if (e != hipSuccess) return finish("usf_corr_bwd_ex_f32", e, (hipStream_t)stream);
@@ -223,7 +222,7 @@ int usf_corr_bwd_ex_f32(const float* x1, const float* x2, const float* gout, lon
 }
 
 long long usf_corr_bwd_ex_scratch(int B, int C, int H, int W, int d) {
-  if (B <= 0 || C <= 0 || H <= 0 || W <= 0 || d < 1 || d > 4 || corr_bwd_fuses_act(d, W)) return 0;
+  if (B <= 0 || C <= 0 || H <= 0 || W <= 0 || d < 1 || d > 4) return 0;
   return (long long)B * (2 * d + 1) * (2 * d + 1) * H * W;
 }
 

@@ -1063,7 +1063,6 @@ long long corr_fwd_workspace(int B, int C, int H, int W, int d) {
 // the prologue spilled 250-600 bytes past the 168-VGPR budget of the
 // 3-waves/SIMD backward. The forward's sign mask (BwdEpi::mask, 6-18 extra
 // VGPRs) is the fused form.
-bool corr_bwd_fuses_act(int, int) { return false; }
 
 long long corr_act_mask_words(int B, int H, int W, int d) {
   if (W % 4 != 0 || d < 1 || d > 4) return 0;

@@ -86,7 +86,6 @@ hipError_t corr_fwd_launch(const float* x1, const float* x2, float* out, int B, 
                            long long workspace_floats = 0);
 // floats of workspace that lets the forward split its channel loop (0: no split)
 long long corr_fwd_workspace(int B, int C, int H, int W, int d);
-bool corr_bwd_fuses_act(int d, int W);
 hipError_t corr_bwd_launch(const float* x1, const float* x2, const float* gout,
                            float* gx1, float* gx2, int B, int C, int H, int W, int d,
                            hipStream_t s, BwdEpi ep);
