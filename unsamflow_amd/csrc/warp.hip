@@ -22,6 +22,7 @@
 // and weights are computed once per lane and reused over its channels. grad_x uses fp32
 // global atomics (global_atomic_add_f32, no CAS loop); grad_flow is a
 // per-lane reduction over channels, written once (deterministic).
+#include <algorithm>
 #include <climits>
 
 #include "usf_common.h"
@@ -258,19 +259,22 @@ __global__ __launch_bounds__(256) void warp_bwd_kernel(const float* __restrict__
 constexpr int GTW = 32, GTH = 8, GCC = 16;
 constexpr int GWX = GTW + 2 * kGatherR + 2, GWY = GTH + 2 * kGatherR + 2;  // source window
 constexpr int GWN = GWX * GWY;
+constexpr int kGList = 8;  // contributors a cell keeps in its list (more: per-chunk rescan)
 
 template <bool BORDER>
 __global__ __launch_bounds__(256) void warp_gx_gather_kernel(const float* __restrict__ flow, long long fbs,
                                                              const float* __restrict__ gout,
                                                              float* __restrict__ gx, int C, int H, int W,
-                                                             int tiles_x, int chunks) {
+                                                             int tiles_x, int cgroups, int cper) {
   constexpr int R = kGatherR;
   __shared__ int spos[GWN];        // (yn - wy0) << 16 | (xw - wx0), or -1: no corner
   __shared__ float swt[4][GWN];    // nw, ne, sw, se weights (0 where masked)
+  __shared__ int lsrc[kGList][256];  // per-cell contributor lists (source offset, weight)
+  __shared__ float lwt[kGList][256];
   const int HW = H * W;
   const int t = threadIdx.x;
   const int tile = blockIdx.x;
-  const int b = blockIdx.y / chunks, chunk = blockIdx.y - b * chunks;
+  const int b = blockIdx.y / cgroups, cgrp = blockIdx.y - b * cgroups;
   const int ty = tile / tiles_x, tx = tile - ty * tiles_x;
   const int x0 = tx * GTW, y0 = ty * GTH;
   const int wx0 = x0 - R - 1, wy0 = y0 - R - 1;  // window origin (source coordinates)
@@ -284,7 +288,8 @@ __global__ __launch_bounds__(256) void warp_gx_gather_kernel(const float* __rest
       const float u = fb[s], v = fb[HW + s];
       if (gather_inlier(u, v)) {
         const Tap tp = make_tap(u, v, sx, sy, H, W, BORDER);
-        // inliers land within R + 1 of the source: relative corner in [0, GWX)
+        // inliers land within R + 1 of the source; a corner left of / above the
+        // window makes pos negative (it reaches no cell of the tile)
         pos = ((tp.yn - wy0) << 16) | (tp.xw - wx0);
         w4[0] = tp.m_nw ? tp.s * tp.e : 0.f;
         w4[1] = tp.m_ne ? tp.s * tp.w : 0.f;
@@ -298,34 +303,59 @@ __global__ __launch_bounds__(256) void warp_gx_gather_kernel(const float* __rest
   }
   __syncthreads();
   const int qx = x0 + (t % GTW), qy = y0 + (t / GTW);
-  if (qx >= W || qy >= H) return;
-  const int c0 = chunk * GCC;
-  const int nc = min(GCC, C - c0);
-  const float* gb = gout + ((size_t)b * C + c0) * HW;
-  float acc[GCC];
+  if (qx >= W || qy >= H) return;  // no barrier below
+  const int rx = qx - wx0, ry = qy - wy0;  // q relative to the window
+  // the sources within R + 1 of q whose corner is q, in a fixed scan order
+  auto scan = [&](auto&& take) {
+    for (int dy = -R - 1; dy <= R + 1; ++dy) {
+      for (int dx = -R - 1; dx <= R + 1; ++dx) {
+        const int i = (ry + dy) * GWX + (rx + dx);
+        const int pos = spos[i];
+        if (pos < 0) continue;
+        const int cx = rx - (pos & 0xFFFF), cy = ry - (pos >> 16);  // q - north-west corner
+        if ((unsigned)cx > 1u || (unsigned)cy > 1u) continue;
+        const float w = swt[cy * 2 + cx][i];
+        if (w == 0.f) continue;
+        take((wy0 + ry + dy) * W + (wx0 + rx + dx), w);
+      }
+    }
+  };
+  int cnt = 0;
+  scan([&](int s, float w) {
+    if (cnt < kGList) {
+      lsrc[cnt][t] = s;
+      lwt[cnt][t] = w;
+    }
+    ++cnt;
+  });
+  const int cbeg = cgrp * cper, cend = min(C, cbeg + cper);
+  const float* gb = gout + (size_t)b * C * HW;
+  float* gq = gx + (size_t)b * C * HW + qy * W + qx;
+  const bool overflow = __any(cnt > kGList);  // converging flow: rescan per channel chunk
+  for (int c0 = cbeg; c0 < cend; c0 += GCC) {
+    float acc[GCC];
 #pragma unroll
-  for (int c = 0; c < GCC; ++c) acc[c] = 0.f;
-  // q relative to the window; sources within R + 1 of q in both axes
-  const int rx = qx - wx0, ry = qy - wy0;
-  for (int dy = -R - 1; dy <= R + 1; ++dy) {
-    for (int dx = -R - 1; dx <= R + 1; ++dx) {
-      const int i = (ry + dy) * GWX + (rx + dx);
-      const int pos = spos[i];
-      if (pos < 0) continue;
-      const int cx = rx - (pos & 0xFFFF), cy = ry - (pos >> 16);  // q - north-west corner
-      if ((unsigned)cx > 1u || (unsigned)cy > 1u) continue;
-      const float w = swt[cy * 2 + cx][i];
-      if (w == 0.f) continue;
-      const int s = (wy0 + ry + dy) * W + (wx0 + rx + dx);
+    for (int c = 0; c < GCC; ++c) acc[c] = 0.f;
+    auto add = [&](int s, float w) {
 #pragma unroll
       for (int c = 0; c < GCC; ++c)
-        if (c < nc) acc[c] = fmaf(w, gb[(size_t)c * HW + s], acc[c]);
+        if (c0 + c < cend) acc[c] = fmaf(w, gb[(size_t)(c0 + c) * HW + s], acc[c]);
+    };
+    if (overflow) {
+      scan(add);
+    } else {
+      // list slot j of every lane at once: no divergence between the lanes'
+      // different source positions (same order as the scan)
+      for (int j = 0; j < kGList; ++j) {
+        if (!__any(j < cnt)) break;
+        const bool has = j < cnt;
+        add(has ? lsrc[j][t] : qy * W + qx, has ? lwt[j][t] : 0.f);
+      }
     }
-  }
-  float* gq = gx + ((size_t)b * C + c0) * HW + qy * W + qx;
 #pragma unroll
-  for (int c = 0; c < GCC; ++c)
-    if (c < nc) gq[(size_t)c * HW] = acc[c];
+    for (int c = 0; c < GCC; ++c)
+      if (c0 + c < cend) gq[(size_t)(c0 + c) * HW] = acc[c];
+  }
 }
 
 // grad_x with the corner scatter pre-summed in LDS. A workgroup owns a 2-D
@@ -554,9 +584,14 @@ void bwd_gather_cs(const float* x, const float* flow, long long fbs, const float
     hipLaunchKernelGGL((warp_bwd_kernel<BORDER, false, true, CS>), grid, block, 0, s, x, flow, fbs, gout,
                        nullptr, gflow, B, C, H, W);
   const int tiles_x = (W + GTW - 1) / GTW, tiles_y = (H + GTH - 1) / GTH;
+  // channel groups only where the tiles alone give few workgroups (L1: 16)
   const int chunks = (C + GCC - 1) / GCC;
-  hipLaunchKernelGGL((warp_gx_gather_kernel<BORDER>), dim3((unsigned)(tiles_x * tiles_y), (unsigned)(B * chunks)),
-                     block, 0, s, flow, fbs, gout, gx, C, H, W, tiles_x, chunks);
+  const long units = (long)tiles_x * tiles_y * B;
+  const int want = (int)std::min<long>(chunks, std::max<long>(1, (512 + units - 1) / units));
+  const int cper = ((chunks + want - 1) / want) * GCC;
+  const int cgroups = (C + cper - 1) / cper;
+  hipLaunchKernelGGL((warp_gx_gather_kernel<BORDER>), dim3((unsigned)(tiles_x * tiles_y), (unsigned)(B * cgroups)),
+                     block, 0, s, flow, fbs, gout, gx, C, H, W, tiles_x, cgroups, cper);
   hipLaunchKernelGGL((warp_bwd_kernel<BORDER, true, false, CS, true>), grid, block, 0, s, x, flow, fbs, gout,
                      gx, nullptr, B, C, H, W);
 }
