@@ -129,7 +129,28 @@ def kernel_report(summary, device, steps, replay=True):
         "method": "algorithmic bytes (SURVEY 8d) / mean duration of the site's launches in the timed region "
                   "(HIP events on the launch stream)",
     }
+    if row["op"] == "warp_bwd" and row["shape"][5]:
+        roof["atomic_floor"] = atomic_floor(row["shape"], row["in_step_us"])
     return rows, roof, {k: round(v, 1) for k, v in per_op.items()}
+
+
+def atomic_floor(shape, mean_us):
+    """The warp backward's grad_x scatter is bound by fp32 atomic throughput:
+    >= 2 atomics per (pixel, channel) after the wave's run merging (north and
+    south corner rows), at the rate tools/probes/atomic_probe.hip measured on the
+    box (profiles/r01_atomic_probe.json). Returns that floor and the site's
+    fraction of it."""
+    path = os.path.join(REPO, "profiles", "r01_atomic_probe.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        probe = json.load(f)
+    B, C, H, W = shape[:4]
+    n = 2 * B * C * H * W
+    gops = max(probe["contig_2_gops"], probe["reuse2_gops"])
+    floor_us = n / (gops * 1e9) * 1e6
+    return {"atomics_per_launch_min": n, "atomic_rate_gops": gops, "floor_us": round(floor_us, 2),
+            "frac_of_floor": round(floor_us / mean_us, 4), "source": "profiles/r01_atomic_probe.json"}
 
 
 SURVEY_CONFIGS = {"cfg1": (2, 32, 64, 128), "cfg2": (8, 128, 32, 104)}  # SURVEY.md §8d configs 1 and 2
