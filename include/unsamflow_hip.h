@@ -262,7 +262,8 @@ int usf_area_pyramid_f32(const float* x, float* out1, float* out2, float* out3, 
  * op 0 = correlation forward tile config, op 1 = correlation backward tile
  * config, op 2 = warp grad_x scatter (0 = wave reduce-by-key + direct global
  * atomics, 1 = LDS-aggregated tiles, 2 / 3 = variant 0 with 4 / 1 channel
- * slices per workgroup, 4 = gather for |flow| < 2 px + scatter for the rest);
+ * slices per workgroup, 4 = gather for |flow| < 2 px + scatter for the rest,
+ * 5 = scatter over vertically adjacent pixel pairs);
  * index -1 restores the built-in choice. Returns the number of
  * variants of `op` (so index range is [0, n)), or USF_EINVAL for an unknown op
  * or out-of-range index. Process-wide; set it before launching, not

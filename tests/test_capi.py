@@ -132,7 +132,7 @@ def test_variant_override_bounds(lib):
     assert n_fwd > 1 and n_bwd > 1
     assert lib.usf_set_variant(0, n_fwd) == -1 and b"bad op" in lib.usf_last_error_string()
     assert lib.usf_set_variant(3, 0) == -1
-    assert lib.usf_set_variant(2, 1) == 5 and lib.usf_set_variant(2, -1) == 5
+    assert lib.usf_set_variant(2, 1) == 6 and lib.usf_set_variant(2, -1) == 6
     assert lib.usf_set_variant(1, n_bwd - 1) == n_bwd
     assert lib.usf_set_variant(1, -1) == n_bwd
 

@@ -338,7 +338,7 @@ def test_corr_every_tile_variant_vs_oracle(hip_device, shape):
         lib.usf_set_variant(1, -1)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5])
 def test_warp_grad_x_scatter_variants(hip_device, variant):
     """Every grad_x variant (reduce-by-key atomics with any channel split,
     LDS-aggregated tiles, the gather with its outlier scatter) matches the
@@ -444,3 +444,21 @@ def test_corr_fwd_channel_split_vs_unsplit_and_oracle(hip_device, shape):
     ops.corr_forward_ex(t1, t2, 4, cat[:, 3:84], leaky_slope=0.1)
     np.testing.assert_allclose(_np(cat[:, 3:84]), _np(torch.nn.functional.leaky_relu(split, 0.1)), atol=0, rtol=0)
     assert float(cat[:, :3].min()) == 7.0 and float(cat[:, 84:].max()) == 7.0
+
+
+@pytest.mark.parametrize("shape,scale", [((2, 8, 64, 208), 1.5), ((1, 4, 65, 130), 3.0), ((2, 4, 64, 208), 0.0)])
+def test_warp_backward_default_large_levels(hip_device, shape, scale):
+    """The default backward at large levels (the pixel-pair scatter: >= 4096 pairs
+    per sample) against the oracle, incl. an odd height and zero flow (every pair
+    merges)."""
+    from unsamflow_amd import ops
+
+    x = hashrng.uniform(shape, 600)
+    flow = hashrng.symmetric((shape[0], 2) + shape[2:], 601, scale) if scale else \
+        np.zeros((shape[0], 2) + shape[2:], np.float32)
+    g = hashrng.normal(shape, 602)
+    for pad in ("border", "zeros"):
+        gx, gf = ops.warp_backward(_dev(x, hip_device), _dev(flow, hip_device), _dev(g, hip_device), pad)
+        rx, rf = warp_backward_np(x, flow, g, pad)
+        np.testing.assert_allclose(_np(gx), rx, atol=1e-4, rtol=1e-5)
+        np.testing.assert_allclose(_np(gf), rf, atol=1e-4, rtol=1e-5)

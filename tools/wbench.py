@@ -48,7 +48,7 @@ def main():
         for fname, fl in flows(B, H, W, dev).items():
             for need_x, need_f in ((True, True), (True, False), (False, True)):
                 # -1: lane-merged scatter (default); 1: LDS-aggregated scatter; 4: gather grad_x
-                for v in ((-1, 1, 4) if need_x else (-1,)):
+                for v in ((-1, 4, 5) if need_x else (-1,)):
                     lib.usf_set_variant(2, v)
                     t = device_time_us(lambda: ops.warp_backward(x, fl, go, "border", need_x, need_f))
                     row = {"shape": [B, C, H, W], "flow": fname, "grad_x": need_x, "grad_flow": need_f,

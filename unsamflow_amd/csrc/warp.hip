@@ -148,6 +148,116 @@ __device__ __forceinline__ void scatter_row(float* gc, int o_w, int o_e, bool m_
   }
 }
 
+// grad_x scatter over vertically adjacent PIXEL PAIRS: lane = (x, rows 2j and
+// 2j + 1). When both pixels hit the same west column and consecutive corner
+// rows (smooth flow), the first pixel's south row and the second's north row
+// are the same cells: the lane adds the two contributions before the wave's
+// reduce-by-key, so a pair scatters 3 corner rows instead of 4 (1.5 atomics per
+// pixel and channel instead of 2). Lanes whose pixels do not line up keep a
+// fourth row (issued only when some lane of the wave needs it).
+__device__ __forceinline__ int row_key(bool ok, int row, int xw, int H, int W, int lane) {
+  // keys alias nothing only for west columns in [-1, W-1]; elsewhere both cells are off-image
+  return ok && xw >= -1 && xw < W && (unsigned)row < (unsigned)H ? row * (W + 1) + xw + 1 : -(lane + 2);
+}
+
+template <bool BORDER, bool WANT_GF, int CS>
+__global__ __launch_bounds__(256) void warp_bwd_pair_kernel(const float* __restrict__ x,
+                                                            const float* __restrict__ flow,
+                                                            long long fbs,
+                                                            const float* __restrict__ gout,
+                                                            float* __restrict__ gx,
+                                                            float* __restrict__ gflow, int B, int C,
+                                                            int H, int W) {
+  constexpr int PXB = 256 / CS;
+  __shared__ float red[4][256];
+  const int HW = H * W, H2 = (H + 1) >> 1;
+  const int t = threadIdx.x;
+  const int slice = t / PXB;
+  const int pl = t - slice * PXB;
+  const int lane = t & 63;
+  int bx, b;
+  warp_block(bx, b);
+  const int pp = bx * PXB + pl;  // pair index over W x ceil(H / 2)
+  const bool v0 = pp < W * H2;
+  const int px = v0 ? pp % W : 0, py = v0 ? 2 * (pp / W) : 0;
+  const bool v1 = v0 && py + 1 < H;
+  const int p0 = py * W + px, p1 = v1 ? p0 + W : p0;
+  const float* fb = flow + b * fbs;
+  Tap t0{}, t1{};
+  if (v0) t0 = make_tap(fb[p0], fb[HW + p0], px, py, H, W, BORDER);
+  if (v1) t1 = make_tap(fb[p1], fb[HW + p1], px, py + 1, H, W, BORDER);
+  if (!v0) t0.m_nw = t0.m_ne = t0.m_sw = t0.m_se = false;
+  if (!v1) t1.m_nw = t1.m_ne = t1.m_sw = t1.m_se = false;
+  const bool merged = v1 && t0.xw == t1.xw && t0.yn + 1 == t1.yn;
+  const bool split = __any(v1 && !merged);  // wave-uniform
+  const bool has_left = pl > 0 && lane != 0;
+  const bool has_right = pl + 1 < PXB && lane != 63;
+  const RowRuns r0 = row_runs(row_key(v0, t0.yn, t0.xw, H, W, lane), t0.m_nw, t0.m_ne, has_left, has_right);
+  const RowRuns r1 = row_runs(row_key(v0, t0.yn + 1, t0.xw, H, W, lane), t0.m_sw, t0.m_se, has_left, has_right);
+  const RowRuns r2 = row_runs(row_key(v1, t1.yn + 1, t1.xw, H, W, lane), t1.m_sw, t1.m_se, has_left, has_right);
+  const bool n1 = v1 && !merged;  // the second pixel's north row on its own
+  RowRuns r3{};
+  if (split) r3 = row_runs(row_key(n1, t1.yn, t1.xw, H, W, lane), t1.m_nw && n1, t1.m_ne && n1, has_left, has_right);
+  const float wnw0 = t0.s * t0.e, wne0 = t0.s * t0.w, wsw0 = t0.n * t0.e, wse0 = t0.n * t0.w;
+  const float wnw1 = t1.s * t1.e, wne1 = t1.s * t1.w, wsw1 = t1.n * t1.e, wse1 = t1.n * t1.w;
+  float dix0 = 0.f, diy0 = 0.f, dix1 = 0.f, diy1 = 0.f;
+  const float* xb = x + (size_t)b * C * HW;
+  const float* gb = gout + (size_t)b * C * HW;
+  float* gxb = gx + (size_t)b * C * HW;
+#pragma unroll 2
+  for (int c = slice; c < C; c += CS) {
+    const float go0 = v0 ? gb[(size_t)c * HW + p0] : 0.f;
+    const float go1 = v1 ? gb[(size_t)c * HW + p1] : 0.f;
+    float* gc = gxb + (size_t)c * HW;
+    scatter_row(gc, t0.o_nw, t0.o_ne, t0.m_nw, t0.m_ne, go0 * wnw0, go0 * wne0, r0);
+    const float vw = merged ? go0 * wsw0 + go1 * wnw1 : go0 * wsw0;
+    const float ve = merged ? go0 * wse0 + go1 * wne1 : go0 * wse0;
+    scatter_row(gc, t0.o_sw, t0.o_se, t0.m_sw, t0.m_se, vw, ve, r1);
+    scatter_row(gc, t1.o_sw, t1.o_se, t1.m_sw, t1.m_se, go1 * wsw1, go1 * wse1, r2);
+    if (split) scatter_row(gc, t1.o_nw, t1.o_ne, t1.m_nw && n1, t1.m_ne && n1, go1 * wnw1, go1 * wne1, r3);
+    if (WANT_GF) {
+      const float* xc = xb + (size_t)c * HW;
+      if (v0) {
+        const float a = t0.m_nw ? xc[t0.o_nw] : 0.f, e = t0.m_ne ? xc[t0.o_ne] : 0.f;
+        const float s = t0.m_sw ? xc[t0.o_sw] : 0.f, d = t0.m_se ? xc[t0.o_se] : 0.f;
+        dix0 += ((e - a) * t0.s + (d - s) * t0.n) * go0;
+        diy0 += ((s - a) * t0.e + (d - e) * t0.w) * go0;
+      }
+      if (v1) {
+        const float a = t1.m_nw ? xc[t1.o_nw] : 0.f, e = t1.m_ne ? xc[t1.o_ne] : 0.f;
+        const float s = t1.m_sw ? xc[t1.o_sw] : 0.f, d = t1.m_se ? xc[t1.o_se] : 0.f;
+        dix1 += ((e - a) * t1.s + (d - s) * t1.n) * go1;
+        diy1 += ((s - a) * t1.e + (d - e) * t1.w) * go1;
+      }
+    }
+  }
+  if (!WANT_GF) return;
+  if (CS > 1) {  // channel slices combined in a fixed order (deterministic)
+    red[0][t] = dix0;
+    red[1][t] = diy0;
+    red[2][t] = dix1;
+    red[3][t] = diy1;
+    __syncthreads();
+    if (slice != 0) return;
+#pragma unroll
+    for (int k = 1; k < CS; ++k) {
+      dix0 += red[0][pl + k * PXB];
+      diy0 += red[1][pl + k * PXB];
+      dix1 += red[2][pl + k * PXB];
+      diy1 += red[3][pl + k * PXB];
+    }
+  }
+  float* gf = gflow + (size_t)b * 2 * HW;
+  if (v0) {
+    gf[p0] = ((dix0 * t0.mx) / (float)(W - 1)) * 2.0f;
+    gf[HW + p0] = ((diy0 * t0.my) / (float)(H - 1)) * 2.0f;
+  }
+  if (v1) {
+    gf[p1] = ((dix1 * t1.mx) / (float)(W - 1)) * 2.0f;
+    gf[HW + p1] = ((diy1 * t1.my) / (float)(H - 1)) * 2.0f;
+  }
+}
+
 // grad_x gather (warp_gx_gather_kernel) covers source pixels whose flow is
 // below kGatherR pixels in both components ("inliers"); the scatter below,
 // with OUTL, adds the rest.
@@ -574,6 +684,19 @@ void bwd_launch_cs(const float* x, const float* flow, long long fbs, const float
                        fbs, gout, gx, gflow, B, C, H, W);
 }
 
+template <bool BORDER, int CS>
+void bwd_pair_cs(const float* x, const float* flow, long long fbs, const float* gout, float* gx,
+                 float* gflow, int B, int C, int H, int W, hipStream_t s) {
+  const int pairs = W * ((H + 1) / 2);
+  const dim3 grid((unsigned)((pairs + 256 / CS - 1) / (256 / CS)), (unsigned)B), block(256);
+  if (gflow)
+    hipLaunchKernelGGL((warp_bwd_pair_kernel<BORDER, true, CS>), grid, block, 0, s, x, flow, fbs, gout, gx,
+                       gflow, B, C, H, W);
+  else
+    hipLaunchKernelGGL((warp_bwd_pair_kernel<BORDER, false, CS>), grid, block, 0, s, x, flow, fbs, gout, gx,
+                       gflow, B, C, H, W);
+}
+
 // grad_x by gather (+ the scatter for |flow| >= kGatherR), grad_flow by the
 // scatter kernel's channel reduction without its grad_x part.
 template <bool BORDER, int CS>
@@ -621,6 +744,22 @@ void bwd_launch_pad(const float* x, const float* flow, long long fbs, const floa
   }
   // the scatter variants accumulate into gx: zero it first (gx is overwritten either way)
   if (gx) (void)hipMemsetAsync(gx, 0, sizeof(float) * (size_t)B * C * H * W, s);
+  // pixel-pair scatter: variant 5, and the default for large levels. Measured at
+  // batch 16 (profiles/ab_r01/warp_pairs.json, grad_x + grad_flow): L4 67 vs
+  // 82 us (zero flow), 50 vs 60 (constant sub-pixel), equal for +-2 / +-8 px
+  // fields; at L2 it halves the workgroups and is slower (52 vs 31 us).
+  const bool pair_default = v < 0 && (long)W * ((H + 1) / 2) >= 4096 && C >= 4;
+  if (gx && (v == 5 || pair_default)) {
+    const long runs64p = (long)B * ((W * ((H + 1) / 2) + 63) / 64);
+    const int csp = (runs64p >= 96 && C >= 4) ? 4 : pick_cs(B, C, W * ((H + 1) / 2));
+    switch (csp) {
+      case 1: bwd_pair_cs<BORDER, 1>(x, flow, fbs, gout, gx, gflow, B, C, H, W, s); break;
+      case 4: bwd_pair_cs<BORDER, 4>(x, flow, fbs, gout, gx, gflow, B, C, H, W, s); break;
+      case 16: bwd_pair_cs<BORDER, 16>(x, flow, fbs, gout, gx, gflow, B, C, H, W, s); break;
+      default: bwd_pair_cs<BORDER, 64>(x, flow, fbs, gout, gx, gflow, B, C, H, W, s); break;
+    }
+    return;
+  }
   // Default: CS = 4 (each wave one 64-pixel run of one channel, so an atomic
   // wave-instruction covers one contiguous row piece) whenever that still gives
   // ~100 workgroups; narrower pixel runs (CS 16/64) only for the tiny levels.
