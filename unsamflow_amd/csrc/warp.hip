@@ -826,6 +826,92 @@ __global__ __launch_bounds__(256) void splat_kernel(const float* __restrict__ fl
   scatter_row(mb, o_sw, o_sw + 1, m_sw, m_se, ax0 * ay1, ax1 * ay1, rs);
 }
 
+// The splat over vertically adjacent pixel pairs (as warp_bwd_pair_kernel): a
+// lane owns rows 2j and 2j + 1 of one column; when both land on the same west
+// column and consecutive (unsaturated) corner rows, the shared row's four
+// weights are added in the lane and the pair scatters 3 rows instead of 4.
+struct SplatTap {
+  int xi, yi;
+  bool m_nw, m_ne, m_sw, m_se, kx, ky;  // ky: yi in [-1, H-1] (not saturated)
+  float ax0, ax1, ay0, ay1;
+};
+template <bool ABS>
+__device__ __forceinline__ SplatTap splat_tap(const float* __restrict__ fb, int p, int px, int py, bool valid,
+                                              int H, int W) {
+#pragma clang fp contract(off)
+  const int HW = H * W;
+  float x = 0.f, y = 0.f;
+  if (valid) {
+    x = ABS ? fb[p] : (float)px + fb[p];
+    y = ABS ? fb[HW + p] : (float)py + fb[HW + p];
+  }
+  SplatTap s;
+  const float fx = floorf(x), fy = floorf(y);
+  const float fx1 = fx + 1.f, fy1 = fy + 1.f;
+  const float wm1 = (float)(W - 1), hm1 = (float)(H - 1);
+  const bool vx0 = fx >= 0.f && fx <= wm1, vx1 = fx1 >= 0.f && fx1 <= wm1;
+  const bool vy0 = valid && fy >= 0.f && fy <= hm1, vy1 = valid && fy1 >= 0.f && fy1 <= hm1;
+  s.ax0 = 1.f - fabsf(x - fx);
+  s.ax1 = 1.f - fabsf(x - fx1);
+  s.ay0 = 1.f - fabsf(y - fy);
+  s.ay1 = 1.f - fabsf(y - fy1);
+  s.xi = fx < -1.f ? -2 : (fx > wm1 ? W : (int)fx);
+  s.yi = fy < -1.f ? -2 : (fy > hm1 ? H : (int)fy);
+  s.kx = s.xi >= -1 && s.xi < W;
+  s.ky = valid && s.yi >= -1 && s.yi < H;
+  s.m_nw = vx0 && vy0;
+  s.m_ne = vx1 && vy0;
+  s.m_sw = vx0 && vy1;
+  s.m_se = vx1 && vy1;
+  return s;
+}
+
+template <bool ABS>
+__global__ __launch_bounds__(256) void splat_pair_kernel(const float* __restrict__ flow, long long fbs,
+                                                         float* __restrict__ map, int H, int W) {
+#pragma clang fp contract(off)
+  const int HW = H * W, H2 = (H + 1) >> 1;
+  const int t = threadIdx.x;
+  const int lane = t & 63;
+  int bx, b;
+  warp_block(bx, b);
+  const int pp = bx * 256 + t;
+  const bool v0 = pp < W * H2;
+  const int px = v0 ? pp % W : 0, py = v0 ? 2 * (pp / W) : 0;
+  const bool v1 = v0 && py + 1 < H;
+  const float* fb = flow + b * fbs;
+  const int p0 = py * W + px;
+  const SplatTap s0 = splat_tap<ABS>(fb, p0, px, py, v0, H, W);
+  const SplatTap s1 = splat_tap<ABS>(fb, v1 ? p0 + W : p0, px, py + 1, v1, H, W);
+  const bool merged = v1 && s0.kx && s0.ky && s1.ky && s0.xi == s1.xi && s0.yi + 1 == s1.yi;
+  const bool split = __any(v1 && !merged);
+  const bool has_left = lane != 0, has_right = lane != 63;
+  auto key = [&](const SplatTap& s, int row, bool rowok) {
+    return rowok && s.kx ? row * (W + 1) + s.xi + 1 : -(lane + 2);
+  };
+  // rows: yi (north, valid iff its corners' row is in the image) and yi + 1
+  const RowRuns r0 = row_runs(key(s0, s0.yi, v0 && s0.yi >= 0 && s0.yi < H), s0.m_nw, s0.m_ne, has_left, has_right);
+  const RowRuns r1 = row_runs(key(s0, s0.yi + 1, v0 && s0.yi + 1 >= 0 && s0.yi + 1 < H), s0.m_sw, s0.m_se,
+                              has_left, has_right);
+  const RowRuns r2 = row_runs(key(s1, s1.yi + 1, v1 && s1.yi + 1 >= 0 && s1.yi + 1 < H), s1.m_sw, s1.m_se,
+                              has_left, has_right);
+  const bool own1 = v1 && !merged;
+  RowRuns r3{};
+  if (split)
+    r3 = row_runs(key(s1, s1.yi, own1 && s1.yi >= 0 && s1.yi < H), s1.m_nw && own1, s1.m_ne && own1,
+                  has_left, has_right);
+  float* mb = map + (size_t)b * HW;
+  const int o0 = s0.yi * W + s0.xi, o1 = s1.yi * W + s1.xi;
+  const int on0 = s0.m_nw || s0.m_ne ? o0 : 0, os0 = s0.m_sw || s0.m_se ? o0 + W : 0;
+  const int on1 = s1.m_nw || s1.m_ne ? o1 : 0, os1 = s1.m_sw || s1.m_se ? o1 + W : 0;
+  scatter_row(mb, on0, on0 + 1, s0.m_nw, s0.m_ne, s0.ax0 * s0.ay0, s0.ax1 * s0.ay0, r0);
+  const float vw = merged ? s0.ax0 * s0.ay1 + s1.ax0 * s1.ay0 : s0.ax0 * s0.ay1;
+  const float ve = merged ? s0.ax1 * s0.ay1 + s1.ax1 * s1.ay0 : s0.ax1 * s0.ay1;
+  scatter_row(mb, os0, os0 + 1, s0.m_sw, s0.m_se, vw, ve, r1);
+  scatter_row(mb, os1, os1 + 1, s1.m_sw, s1.m_se, s1.ax0 * s1.ay1, s1.ax1 * s1.ay1, r2);
+  if (split) scatter_row(mb, on1, on1 + 1, s1.m_nw && own1, s1.m_ne && own1, s1.ax0 * s1.ay0, s1.ax1 * s1.ay0, r3);
+}
+
 // occ = clamp(map, 0, 1) < th ? 1 : 0, in place (get_occu_mask_backward :124-126)
 __global__ __launch_bounds__(256) void occ_threshold_kernel(float* __restrict__ m, long long n,
                                                             float th) {
@@ -859,6 +945,15 @@ hipError_t splat_launch(const float* flow, long long fbs, float* map, int B, int
                         bool absolute, hipStream_t s) {
   hipError_t e = hipMemsetAsync(map, 0, (size_t)B * H * W * sizeof(float), s);
   if (e != hipSuccess) return e;
+  const long pairs = (long)W * ((H + 1) / 2);
+  if (pairs >= 4096 && variant_override(2) != 0) {  // pixel pairs (as the warp backward)
+    const dim3 grid((unsigned)((pairs + 255) / 256), (unsigned)B);
+    if (absolute)
+      hipLaunchKernelGGL((splat_pair_kernel<true>), grid, dim3(256), 0, s, flow, fbs, map, H, W);
+    else
+      hipLaunchKernelGGL((splat_pair_kernel<false>), grid, dim3(256), 0, s, flow, fbs, map, H, W);
+    return hipGetLastError();
+  }
   const dim3 grid((unsigned)((H * W + 255) / 256), (unsigned)B);
   if (absolute)
     hipLaunchKernelGGL((splat_kernel<true>), grid, dim3(256), 0, s, flow, fbs, map, H, W);
