@@ -107,9 +107,9 @@ int usf_corr_bwd_f32(const float* x1, const float* x2, const float* gout,
  * floats): when it holds usf_corr_fwd_workspace(B,C,H,W,d) floats, small
  * levels split the channel loop over more workgroups and reduce the partials
  * in a fixed order (deterministic); otherwise the unsplit kernel runs.
- * act_mask (nullable; act = USF_ACT_LEAKY_RELU and W % 4 == 0 only): also
- * write the sign mask of the activated output, usf_corr_act_mask_words
- * 64-bit words laid out [B][2d+1][H][W/4], bit 4*dx + (x % 4) of word
+ * act_mask (nullable; act = USF_ACT_LEAKY_RELU only): also write the sign
+ * mask of the activated output, usf_corr_act_mask_words 64-bit words laid
+ * out [B][2d+1][H][ceil(W/4)], bit 4*dx + (x % 4) of word
  * (b, dy, y, x/4) = (out at (b, dy*(2d+1)+dx, y, x) > 0). Pass it to
  * usf_corr_bwd_ex_f32 to apply the LeakyReLU derivative without re-reading
  * the activated output. */
@@ -118,7 +118,7 @@ int usf_corr_fwd_ex_f32(const float* x1, const float* x2, float* out, long long 
                         long long workspace_floats, int B, int C, int H, int W, int d,
                         void* stream);
 
-/* 64-bit words of the sign mask at this shape (0: unsupported, W % 4 != 0). */
+/* 64-bit words of the sign mask at this shape (0: bad arguments). */
 long long usf_corr_act_mask_words(int B, int H, int W, int d);
 
 /* Floats of workspace usf_corr_fwd_ex_f32 uses at this shape (0: no split). */
@@ -130,7 +130,7 @@ long long usf_corr_fwd_workspace(int B, int C, int H, int W, int d);
  * is applied first -- torch's leaky_relu_backward on the result, as for the
  * in-place module -- in one dense pass into `scratch` (caller-provided,
  * usf_corr_bwd_ex_scratch(B,C,H,W,d) floats; unused when act_out is NULL).
- * With act_mask != NULL (the forward's sign mask; W % 4 == 0) the same
+ * With act_mask != NULL (the forward's sign mask) the same
  * derivative is applied inside the backward kernel's gradient loads instead:
  * act_out and scratch are ignored and no extra pass runs. */
 int usf_corr_bwd_ex_f32(const float* x1, const float* x2, const float* gout, long long g_bstride,

@@ -83,11 +83,9 @@ def test_no_torch_types_in_abi():
         (lambda L: L.usf_corr_fwd_f32(1, 1, 1, 1, 70000, 200, 200, 4, None), "too large"),
         (lambda L: L.usf_corr_fwd_ex_f32(1, 1, 1, 10, 1, 0.1, None, None, 0, 2, 4, 4, 4, 4, None), "out batch stride"),
         (lambda L: L.usf_corr_fwd_ex_f32(1, 1, 1, 81 * 16, 7, 0.1, None, None, 0, 2, 4, 4, 4, 4, None), "unknown act"),
-        (lambda L: L.usf_corr_fwd_ex_f32(1, 1, 1, 81 * 20, 1, 0.1, 1, None, 0, 2, 4, 4, 5, 4, None), "act_mask needs"),
         (lambda L: L.usf_corr_fwd_ex_f32(1, 1, 1, 81 * 16, 0, 0.1, 1, None, 0, 2, 4, 4, 4, 4, None), "act_mask needs"),
         (lambda L: L.usf_corr_bwd_ex_f32(1, 1, 1, 10, None, None, 0.1, None, 1, 1, 2, 4, 4, 4, 4, None), "gradient batch stride"),
         (lambda L: L.usf_corr_bwd_ex_f32(1, 1, 1, 81 * 20, 1, None, 0.1, None, 1, 1, 2, 4, 4, 5, 4, None), "scratch"),
-        (lambda L: L.usf_corr_bwd_ex_f32(1, 1, 1, 81 * 20, None, 1, 0.1, None, 1, 1, 2, 4, 4, 5, 4, None), "act_mask needs"),
         (lambda L: L.usf_flow_upsample_f32(1, 1, 1, 2, 4, 4, 0, None), "bad factor"),
         (lambda L: L.usf_flow_upsample_bwd_f32(None, 1, 1, 2, 4, 4, 2, None), "null pointer"),
         (lambda L: L.usf_splat_map_f32(1, 2 * 16, 1, 0, 4, 4, 0, None), "non-positive"),

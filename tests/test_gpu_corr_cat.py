@@ -49,10 +49,12 @@ def test_corr_leaky_cat_matches_composition(hip_device, B, C, H, W, n_pairs):
         np.testing.assert_allclose(a.cpu().numpy(), b.cpu().numpy(), atol=1e-6, rtol=1e-6)
 
 
-@pytest.mark.parametrize("B,C,H,W", [(2, 32, 64, 208), (2, 64, 32, 104), (8, 96, 16, 52), (1, 8, 5, 4), (3, 16, 7, 12)])
+@pytest.mark.parametrize("B,C,H,W", [(2, 32, 64, 208), (2, 64, 32, 104), (8, 96, 16, 52), (1, 8, 5, 4), (3, 16, 7, 12),
+                                     (16, 192, 4, 13), (16, 128, 8, 26), (2, 8, 3, 5), (1, 4, 9, 1)])
 def test_sign_mask_derivative_equals_dense_pass(hip_device, B, C, H, W):
     """The forward's LeakyReLU sign mask (epilogue, or the mask kernel after the
-    channel-split reduce at (8, 96, 16, 52)) equals (activated output > 0) bit
+    channel-split reduce at (8, 96, 16, 52) and the KITTI L0/L1 shapes; widths
+    that are not a multiple of 4 included) equals (activated output > 0) bit
     for bit, and the backward that applies the derivative from it inside its
     gradient loads gives the same gradients, bit for bit, as the dense
     derivative pass over the activated output."""
@@ -63,10 +65,12 @@ def test_sign_mask_derivative_equals_dense_pass(hip_device, B, C, H, W):
     buf = torch.zeros((B, 81 + 34, H, W), device=hip_device)
     out = buf[:, :81]
     mask = ops.corr_act_mask(B, H, W, 4, hip_device)
-    assert mask is not None and tuple(mask.shape) == (B, 9, H, W // 4)
+    W4 = (W + 3) // 4
+    assert mask is not None and tuple(mask.shape) == (B, 9, H, W4)
     ops.corr_forward_ex(x1, x2, 4, out, 0.1, act_mask=mask)
     # expected words from the activated output: bit 4 dx + x % 4 of word (b, dy, y, x // 4)
-    pos = (out > 0).view(B, 9, 9, H, W // 4, 4).to(torch.int64)  # b, dy, dx, y, quad, i
+    padded = torch.nn.functional.pad((out > 0).to(torch.int64), (0, 4 * W4 - W))
+    pos = padded.view(B, 9, 9, H, W4, 4)  # b, dy, dx, y, quad, i
     shifts = (4 * torch.arange(9, device=hip_device).view(1, 1, 9, 1, 1, 1)
               + torch.arange(4, device=hip_device).view(1, 1, 1, 1, 1, 4))
     want = (pos << shifts).sum(dim=(2, 5))

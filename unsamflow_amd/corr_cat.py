@@ -8,9 +8,9 @@ into its channel slice of the concat buffer (usf_corr_fwd_ex_f32: output batch
 stride + activation epilogue), so the 81-channel cost map is neither written
 twice (activation pass) nor copied (cat). Backward reads its gradient from the
 concat gradient's slice (batch stride) and applies the LeakyReLU derivative:
-from the sign mask the forward's epilogue wrote (W % 4 == 0: inside the
-backward kernel's gradient loads, no extra pass), else in one dense pass over
-the activated output (usf_corr_bwd_ex_f32); the extras' gradients are views.
+from the sign mask the forward's epilogue wrote, inside the backward kernel's
+gradient loads (usf_corr_bwd_ex_f32; no dense derivative pass); the extras'
+gradients are views.
 """
 from __future__ import annotations
 

@@ -136,8 +136,8 @@ int usf_corr_fwd_ex_f32(const float* x1, const float* x2, float* out, long long 
     set_error("usf_corr_fwd_ex_f32: unknown act %d", act);
     return USF_EINVAL;
   }
-  if (act_mask && (act != USF_ACT_LEAKY_RELU || corr_act_mask_words(B, H, W, d) == 0)) {
-    set_error("usf_corr_fwd_ex_f32: act_mask needs act = LeakyReLU and W %% 4 == 0 (W=%d)", W);
+  if (act_mask && act != USF_ACT_LEAKY_RELU) {
+    set_error("usf_corr_fwd_ex_f32: act_mask needs act = LeakyReLU (act=%d)", act);
     return USF_EINVAL;
   }
   if (const int pe = pre_check("usf_corr_fwd_ex_f32", (hipStream_t)stream)) return pe;
@@ -189,10 +189,6 @@ int usf_corr_bwd_ex_f32(const float* x1, const float* x2, const float* gout, lon
     return USF_EINVAL;
   }
   if (act_mask) {  // derivative from the forward's sign mask, inside the backward's g loads
-    if (corr_act_mask_words(B, H, W, d) == 0) {
-      set_error("usf_corr_bwd_ex_f32: act_mask needs W %% 4 == 0 (W=%d)", W);
-      return USF_EINVAL;
-    }
     if (const int pe = pre_check("usf_corr_bwd_ex_f32", (hipStream_t)stream)) return pe;
     BwdEpi ep{g_bstride};
     ep.mask = act_mask;

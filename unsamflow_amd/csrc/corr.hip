@@ -426,18 +426,19 @@ __global__ __launch_bounds__(64 * NDY) void corr_fwd_kernel(const float* __restr
         if (xb + i < W) o[i] = epi(acc[dx][i]);
     }
   }
-  if (leaky && ep.mask && (W & 3) == 0 && xb < W) {
+  if (leaky && ep.mask && xb < W) {
     // sign bits of this lane's activated outputs, one word per 4-pixel quad
-    // (the same test as the epilogue's: v = acc / C > 0)
-    unsigned long long* mw = ep.mask + ((size_t)(b * K + dy) * H + y) * (W >> 2) + (xb >> 2);
+    // (the same test as the epilogue's: v = acc / C > 0); bits past W stay 0
+    unsigned long long* mw = ep.mask + ((size_t)(b * K + dy) * H + y) * ((W + 3) >> 2) + (xb >> 2);
 #pragma unroll
     for (int j = 0; j < PX / 4; ++j) {
+      if (xb + 4 * j >= W) break;
       unsigned long long bits = 0;
 #pragma unroll
       for (int dx = 0; dx < K; ++dx)
 #pragma unroll
         for (int i = 0; i < 4; ++i)
-          bits |= (unsigned long long)(acc[dx][4 * j + i] / cf > 0.f) << (4 * dx + i);
+          bits |= (unsigned long long)(xb + 4 * j + i < W && acc[dx][4 * j + i] / cf > 0.f) << (4 * dx + i);
       mw[j] = bits;
     }
   }
@@ -451,7 +452,7 @@ __global__ __launch_bounds__(256) void corr_act_mask_kernel(const float* __restr
                                                             long long obs,
                                                             unsigned long long* __restrict__ mask,
                                                             int B, int H, int W) {
-  const int W4 = W >> 2;
+  const int W4 = (W + 3) >> 2;
   const long long n = (long long)B * K * H * W4;
   const long long t = (long long)blockIdx.x * 256 + threadIdx.x;
   if (t >= n) return;
@@ -465,7 +466,8 @@ __global__ __launch_bounds__(256) void corr_act_mask_kernel(const float* __restr
 #pragma unroll
   for (int dx = 0; dx < K; ++dx)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) bits |= (unsigned long long)(o[(size_t)dx * H * W + i] > 0.f) << (4 * dx + i);
+    for (int i = 0; i < 4; ++i)
+      if (4 * qd + i < W) bits |= (unsigned long long)(o[(size_t)dx * H * W + i] > 0.f) << (4 * dx + i);
   mask[t] = bits;
 }
 
@@ -518,7 +520,7 @@ hipError_t launch_fwd_v(const float* x1, const float* x2, float* out, int B, int
     if (ep.act && ep.mask) {
       const hipError_t e2 = hipGetLastError();
       if (e2 != hipSuccess) return e2;
-      const long long n = (long long)B * F::K * H * (W / 4);
+      const long long n = (long long)B * F::K * H * ((W + 3) / 4);
       hipLaunchKernelGGL(corr_act_mask_kernel<F::K>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
                          out, ep.out_bstride, ep.mask, B, H, W);
     }
@@ -678,8 +680,8 @@ __device__ __forceinline__ void corr_bwd_tile(float* sm, const float* __restrict
   // raw buffer descriptors over this sample's K*K planes: 16-byte loads with a
   // 32-bit offset (one VGPR per address instead of a 64-bit pointer pair)
   const auto grs = plane_buf(gb, K * K * HW * 4);
-  // AM: the forward's LeakyReLU sign mask of sample b ([dy][y][x/4] words)
-  const int W4 = W >> 2;
+  // AM: the forward's LeakyReLU sign mask of sample b ([dy][y][ceil(W/4)] words)
+  const int W4 = (W + 3) >> 2;
   const auto mrs = AM ? __builtin_amdgcn_make_buffer_rsrc(
                             const_cast<unsigned long long*>(ep.mask + (size_t)b * K * H * W4), 0,
                             K * H * W4 * 8, kRsrcFlags)
@@ -694,7 +696,7 @@ __device__ __forceinline__ void corr_bwd_tile(float* sm, const float* __restrict
   // load is clamped into the row and the lanes at the image edge pick their
   // elements out of it by index.
   float gv[DYW][K][PX];
-  static_assert(!AM || (PX == 4 && V == 4 && K <= 16), "sign-mask derivative: 4-pixel runs, W % 4 == 0");
+  static_assert(!AM || (PX == 4 && K <= 16), "sign-mask derivative: 4-pixel runs (xb % 4 == 0)");
 #pragma unroll
   for (int t = 0; t < DYW; ++t) {
     const int dy = wave * DYW + t;
@@ -748,7 +750,12 @@ __device__ __forceinline__ void corr_bwd_tile(float* sm, const float* __restrict
         for (int i = 0; i < PX; ++i) {
           const int xx = G2 ? xb + i - dx + D : xb + i;
           const bool ok = rowok && (unsigned)xx < (unsigned)W;
-          const float v = buf_load1(grs, (k * HW + (ok ? yy * W + xx : 0)) * 4);
+          float v = buf_load1(grs, (k * HW + (ok ? yy * W + xx : 0)) * 4);
+          if constexpr (AM) {  // as in the 16-byte path: pixel xb + ei, compile-time word and bit
+            const int ei = G2 ? i - dx + D : i;
+            const bool pos = (mw[(ei + 4) >> 2] >> (4 * dx + (ei & 3))) & 1ull;
+            v = pos ? v : v * ep.slope;
+          }
           gv[t][dx][i] = ok ? v : 0.f;
         }
       }
@@ -929,14 +936,14 @@ hipError_t launch_bwd_mode(const float* x1, const float* x2, const float* g, flo
   groups = max(1, min(groups, (C + CC - 1) / CC));
   const int cg = round_up((C + groups - 1) / groups, CC);
   dim3 grid(tiles_x * tiles_y, (C + cg - 1) / cg, B * dirs);
-  if constexpr (V == 4 && PX == 4) {
+  if constexpr (PX == 4) {
     if (ep.mask) {
       hipLaunchKernelGGL((corr_bwd_kernel<D, PX, SEGX, NW, CC, V, MODE, true>), grid, dim3(F::NT), 0, s,
                          x1, x2, g, gx1, gx2, B, C, H, W, tiles_x, cg, ep);
       return hipGetLastError();
     }
   }
-  if (ep.mask) return hipErrorInvalidValue;  // the sign mask needs W % 4 == 0 (capi checks)
+  if (ep.mask) return hipErrorInvalidValue;  // 4-pixel runs only
   hipLaunchKernelGGL((corr_bwd_kernel<D, PX, SEGX, NW, CC, V, MODE, false>), grid, dim3(F::NT), 0, s, x1,
                      x2, g, gx1, gx2, B, C, H, W, tiles_x, cg, ep);
   return hipGetLastError();
@@ -1065,8 +1072,8 @@ long long corr_fwd_workspace(int B, int C, int H, int W, int d) {
 // VGPRs) is the fused form.
 
 long long corr_act_mask_words(int B, int H, int W, int d) {
-  if (W % 4 != 0 || d < 1 || d > 4) return 0;
-  return (long long)B * (2 * d + 1) * H * (W / 4);
+  if (d < 1 || d > 4) return 0;
+  return (long long)B * (2 * d + 1) * H * ((W + 3) / 4);
 }
 
 hipError_t corr_bwd_launch(const float* x1, const float* x2, const float* gout, float* gx1,

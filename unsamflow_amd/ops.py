@@ -354,11 +354,11 @@ def _plane_slice_stride(name: str, t: torch.Tensor, shape) -> int:
 
 def corr_act_mask(B: int, H: int, W: int, max_displacement: int, device) -> torch.Tensor | None:
     """An empty LeakyReLU sign mask for :func:`corr_forward_ex` (int64 words,
-    [B,2d+1,H,W/4]), or None where the layout needs W % 4 == 0 and W is not."""
+    [B,2d+1,H,ceil(W/4)])."""
     n = int(_lib.load().usf_corr_act_mask_words(B, H, W, int(max_displacement)))
     if n == 0:
         return None
-    return torch.empty((B, 2 * int(max_displacement) + 1, H, W // 4), device=device, dtype=torch.int64)
+    return torch.empty((B, 2 * int(max_displacement) + 1, H, (W + 3) // 4), device=device, dtype=torch.int64)
 
 
 def corr_forward_ex(x1: torch.Tensor, x2: torch.Tensor, max_displacement: int, out: torch.Tensor,
