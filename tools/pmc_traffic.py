@@ -72,9 +72,9 @@ def main():
         pos += prefix.get(op, 0)
         if op == "corr_bwd_leaky" and lib.usf_corr_act_mask_words(key[0], key[2], key[3], 4) > 0:
             # sign-mask path: one backward kernel per launch, after the launcher's
-            # one forward (+ the split forward's reduce and mask kernels)
+            # one forward (+ the split forward's reduce-and-mask kernel)
             k = 1
-            pos += 3 if lib.usf_corr_fwd_workspace(*key[:4], 4) > 0 else 1
+            pos += 2 if lib.usf_corr_fwd_workspace(*key[:4], 4) > 0 else 1
         fk = statistics.median(sum(uf[pos + j * k + i] for i in range(k)) for j in range(n))
         wk = statistics.median(sum(uw[pos + j * k + i] for i in range(k)) for j in range(n))
         pos += k * n
