@@ -70,11 +70,11 @@ def main():
         if op == "corr_fwd" and lib.usf_corr_fwd_workspace(*key[:4], 4) > 0:
             k = 2
         pos += prefix.get(op, 0)
-        if op == "corr_bwd_leaky" and lib.usf_corr_act_mask_words(key[0], key[2], key[3], 4) > 0:
-            # sign-mask path: one backward kernel per launch, after the launcher's
-            # one forward (+ the split forward's reduce-and-mask kernel)
+        if op == "corr_bwd_leaky" and lib.usf_corr_fwd_workspace(*key[:4], 4) == 0:
+            # sign-mask path (unsplit forward): one backward kernel per launch,
+            # after the launcher's one forward kernel
             k = 1
-            pos += 2 if lib.usf_corr_fwd_workspace(*key[:4], 4) > 0 else 1
+            pos += 1
         fk = statistics.median(sum(uf[pos + j * k + i] for i in range(k)) for j in range(n))
         wk = statistics.median(sum(uw[pos + j * k + i] for i in range(k)) for j in range(n))
         pos += k * n
@@ -87,7 +87,7 @@ def main():
         if op.startswith("corr"):
             alg = corr_bytes(*key[:4], backward=op.startswith("corr_bwd"))
             if op == "corr_bwd_leaky":
-                words = lib.usf_corr_act_mask_words(B, H, W, 4)
+                words = lib.usf_corr_act_mask_words(B, H, W, 4) if lib.usf_corr_fwd_workspace(B, C, H, W, 4) == 0 else 0
                 # the derivative's input: the sign mask, else the activated output
                 alg += 8 * words if words else 4 * B * H * W * 81
         elif op == "convex_up":

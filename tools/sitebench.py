@@ -63,7 +63,8 @@ def alg_bytes(op, key):
     if op == "corr_bwd":
         return 4 * B * H * W * (81 + 4 * C)
     if op == "corr_bwd_leaky":  # + the derivative's input: the sign mask, else the activated output
-        words = _lib.load().usf_corr_act_mask_words(B, H, W, 4)
+        lib = _lib.load()
+        words = lib.usf_corr_act_mask_words(B, H, W, 4) if lib.usf_corr_fwd_workspace(B, C, H, W, 4) == 0 else 0
         return 4 * B * H * W * (81 + 4 * C) + (8 * words if words else 4 * B * H * W * 81)
     if op == "warp_fwd":
         return 4 * B * H * W * (2 * C + 2)

@@ -9,8 +9,9 @@ stride + activation epilogue), so the 81-channel cost map is neither written
 twice (activation pass) nor copied (cat). Backward reads its gradient from the
 concat gradient's slice (batch stride) and applies the LeakyReLU derivative:
 from the sign mask the forward's epilogue wrote, inside the backward kernel's
-gradient loads (usf_corr_bwd_ex_f32; no dense derivative pass); the extras'
-gradients are views.
+gradient loads (usf_corr_bwd_ex_f32), or -- at the small levels whose forward
+splits its channel loop -- in one dense pass over the activated output; the
+extras' gradients are views.
 """
 from __future__ import annotations
 
@@ -32,7 +33,7 @@ class CorrLeakyCatFunction(Function):
         off = 0
         masks = []
         for a, b in pairs:
-            m = ops.corr_act_mask(B, H, W, max_displacement, a.device)
+            m = ops.corr_act_mask(B, H, W, max_displacement, a.device, C=a.shape[1])
             ops.corr_forward_ex(a, b, max_displacement, buf[:, off:off + K2], slope, act_mask=m)
             masks.append(m)
             off += K2

@@ -444,14 +444,14 @@ __global__ __launch_bounds__(64 * NDY) void corr_fwd_kernel(const float* __restr
   }
 }
 
-// The channel-split forward's reduce with the sign mask (FwdEpi::mask): one
-// thread per mask word (b, dy, y, 4-pixel quad) sums the 36 outputs' partials
-// in group order (as corr_fwd_reduce_kernel), applies the epilogue and writes
-// the outputs and the word -- one kernel, no second pass over the outputs.
+// The sign mask of FwdEpi::mask from the activated output itself, for the
+// channel-split forward (its reduce kernel applies the epilogue element-wise):
+// one thread per (b, dy, y, quad) reads the 9 dx planes' 4-pixel runs.
 template <int K>
-__global__ __launch_bounds__(256) void corr_fwd_reduce_mask_kernel(const float* __restrict__ part,
-                                                                   float* __restrict__ out, FwdEpi ep,
-                                                                   int G, int B, int H, int W, int C) {
+__global__ __launch_bounds__(256) void corr_act_mask_kernel(const float* __restrict__ out,
+                                                            long long obs,
+                                                            unsigned long long* __restrict__ mask,
+                                                            int B, int H, int W) {
   const int W4 = (W + 3) >> 2;
   const long long n = (long long)B * K * H * W4;
   const long long t = (long long)blockIdx.x * 256 + threadIdx.x;
@@ -461,25 +461,14 @@ __global__ __launch_bounds__(256) void corr_fwd_reduce_mask_kernel(const float* 
   const int y = (int)(row % H);
   const int dy = (int)((row / H) % K);
   const int b = (int)(row / ((long long)H * K));
-  const long long HW = (long long)H * W, KHW = (long long)K * K * HW, per = (long long)B * KHW;
-  const float cf = (float)C;
+  const float* o = out + (size_t)b * obs + (size_t)dy * K * H * W + (size_t)y * W + 4 * qd;
   unsigned long long bits = 0;
 #pragma unroll
-  for (int dx = 0; dx < K; ++dx) {
-    const long long kp = (long long)(dy * K + dx) * HW + (long long)y * W;
+  for (int dx = 0; dx < K; ++dx)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int x = 4 * qd + i;
-      if (x >= W) break;
-      const long long idx = b * KHW + kp + x;
-      float s = part[idx];
-      for (int g = 1; g < G; ++g) s += part[g * per + idx];
-      const float v = s / cf;
-      out[b * ep.out_bstride + kp + x] = v > 0.f ? v : v * ep.slope;
-      bits |= (unsigned long long)(v > 0.f) << (4 * dx + i);
-    }
-  }
-  ep.mask[t] = bits;
+    for (int i = 0; i < 4; ++i)
+      if (4 * qd + i < W) bits |= (unsigned long long)(o[(size_t)dx * H * W + i] > 0.f) << (4 * dx + i);
+  mask[t] = bits;
 }
 
 // out[b * obs + k * HW + p] = epilogue(sum_g part[g][b][k][p] / C), g in order
@@ -526,13 +515,18 @@ hipError_t launch_fwd_v(const float* x1, const float* x2, float* out, int B, int
     if (e != hipSuccess) return e;
     const int KHW = F::K * F::K * H * W;
     const long long per = (long long)B * KHW;
-    if (ep.act && ep.mask) {  // reduce + epilogue + sign mask in one kernel
+    hipLaunchKernelGGL(corr_fwd_reduce_kernel, dim3((unsigned)((per + 1023) / 1024)), dim3(256), 0, s,
+                       ep.part, out, ep, ep.groups, B, KHW, C);
+    if (ep.act && ep.mask) {
+      // a thread-per-word reduce that also writes the mask was measured 4x
+      // slower at L0/L1 (59 vs 15 us: 36 x G dependent partial loads per
+      // thread); the element-wise reduce + this pass keeps the ABI complete,
+      // and the decoder (corr_cat.py) uses the dense derivative at split levels
+      const hipError_t e2 = hipGetLastError();
+      if (e2 != hipSuccess) return e2;
       const long long n = (long long)B * F::K * H * ((W + 3) / 4);
-      hipLaunchKernelGGL(corr_fwd_reduce_mask_kernel<F::K>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
-                         s, ep.part, out, ep, ep.groups, B, H, W, C);
-    } else {
-      hipLaunchKernelGGL(corr_fwd_reduce_kernel, dim3((unsigned)((per + 1023) / 1024)), dim3(256), 0, s,
-                         ep.part, out, ep, ep.groups, B, KHW, C);
+      hipLaunchKernelGGL(corr_act_mask_kernel<F::K>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
+                         out, ep.out_bstride, ep.mask, B, H, W);
     }
   }
   return hipGetLastError();

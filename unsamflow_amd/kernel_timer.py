@@ -154,7 +154,7 @@ def site_launcher(op: str, key, device, seed: int = 0):
         cat = torch.randn(B, 81 + C + 2, H, W, device=device, generator=g)
         act = torch.nn.functional.leaky_relu(torch.randn(B, 81 + C + 2, H, W, device=device, generator=g), 0.1)
         # as corr_cat runs it: the forward's sign mask where W % 4 == 0, else the dense pass
-        mask = ops.corr_act_mask(B, H, W, 4, device)
+        mask = ops.corr_act_mask(B, H, W, 4, device, C=C)
         if mask is not None:
             ops.corr_forward_ex(x1, x2, 4, act[:, :81], 0.1, act_mask=mask)
         return lambda: ops.corr_backward_ex(x1, x2, cat[:, :81], 4, key[4], key[5], act_out=act[:, :81],

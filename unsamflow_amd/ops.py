@@ -352,10 +352,16 @@ def _plane_slice_stride(name: str, t: torch.Tensor, shape) -> int:
     return s[0] if B > 1 else K * H * W
 
 
-def corr_act_mask(B: int, H: int, W: int, max_displacement: int, device) -> torch.Tensor | None:
+def corr_act_mask(B: int, H: int, W: int, max_displacement: int, device, C: int | None = None
+                  ) -> torch.Tensor | None:
     """An empty LeakyReLU sign mask for :func:`corr_forward_ex` (int64 words,
-    [B,2d+1,H,ceil(W/4)])."""
-    n = int(_lib.load().usf_corr_act_mask_words(B, H, W, int(max_displacement)))
+    [B,2d+1,H,ceil(W/4)]). With ``C``: None where the forward splits its channel
+    loop (small levels), whose mask would cost an extra pass over the output --
+    there the backward's dense derivative pass is cheaper."""
+    lib = _lib.load()
+    if C is not None and int(lib.usf_corr_fwd_workspace(B, C, H, W, int(max_displacement))) > 0:
+        return None
+    n = int(lib.usf_corr_act_mask_words(B, H, W, int(max_displacement)))
     if n == 0:
         return None
     return torch.empty((B, 2 * int(max_displacement) + 1, H, (W + 3) // 4), device=device, dtype=torch.int64)
