@@ -35,3 +35,13 @@ def test_default_backward_tile_occupancy(corr_resources):
     for name, vgpr, lds, _ in default:
         assert vgpr <= 168, (name, vgpr)
         assert lds <= 40 * 1024, (name, lds)
+
+
+def test_large_level_forward_occupancy(corr_resources):
+    """The L3/L4 forward tile <d=4, PX=4, SEGX=8, NDY=9, CC=4> keeps its 7
+    waves/SIMD with the sign-mask epilogue (a per-bit bounds test in the
+    epilogue once raised it from 65 to 101 VGPRs and slowed L4 by ~25%)."""
+    fwd = [r for r in corr_resources if "corr_fwd_kernelILi4ELi4ELi8ELi9ELi4E" in r[0]]
+    assert fwd, "large-level forward instantiation missing"
+    for name, vgpr, _, _ in fwd:
+        assert vgpr <= 72, (name, vgpr)

@@ -430,16 +430,22 @@ __global__ __launch_bounds__(64 * NDY) void corr_fwd_kernel(const float* __restr
     // sign bits of this lane's activated outputs, one word per 4-pixel quad
     // (the same test as the epilogue's: v = acc / C > 0); bits past W stay 0
     unsigned long long* mw = ep.mask + ((size_t)(b * K + dy) * H + y) * ((W + 3) >> 2) + (xb >> 2);
+    // one bit per dx nibble, replicated: masks the columns past W of a partial quad
+    constexpr unsigned long long kRep = [] {
+      unsigned long long r = 0;
+      for (int dx = 0; dx < K; ++dx) r |= 1ull << (4 * dx);
+      return r;
+    }();
 #pragma unroll
     for (int j = 0; j < PX / 4; ++j) {
-      if (xb + 4 * j >= W) break;
       unsigned long long bits = 0;
 #pragma unroll
       for (int dx = 0; dx < K; ++dx)
 #pragma unroll
         for (int i = 0; i < 4; ++i)
-          bits |= (unsigned long long)(xb + 4 * j + i < W && acc[dx][4 * j + i] / cf > 0.f) << (4 * dx + i);
-      mw[j] = bits;
+          bits |= (unsigned long long)(acc[dx][4 * j + i] / cf > 0.f) << (4 * dx + i);
+      const int nv = W - (xb + 4 * j);  // valid columns of this quad (> 0 for quads in the row)
+      if (nv > 0) mw[j] = nv >= 4 ? bits : bits & (kRep * ((1ull << nv) - 1));
     }
   }
 }
