@@ -7,8 +7,9 @@ decoder-warp calls at batch 16 through the HIP library; --per-direction: the
 reference's two batch-8 passes) -> unFlowLoss (8 loss warps) -> backward ->
 clip_grad_norm_ -> Adam ->
 OneCycleLR, on B=8 synthetic U[0,1) frame pairs per GPU (kitti_base.json),
-random-init weights. N>1: one process per GPU (torchrun), DDP over RCCL
-("nccl"), B=8 per rank (weak scaling).
+random-init weights. N>1: one process per GPU, DDP over RCCL ("nccl"), B=8
+per rank (weak scaling); under torchrun the ranks come from its environment,
+otherwise ``--gpus N`` starts the N rank processes itself (launch_ranks).
 
 Output: ONE JSON line on rank 0 with the driver's contract fields plus
 * ``roofline`` — the dominant hot-path call site (largest summed time per
@@ -33,6 +34,7 @@ Output: ONE JSON line on rank 0 with the driver's contract fields plus
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
                        [--config kitti|sintel_mf] [--no-cpu-baseline]
+       python bench.py --device cpu --gpus 2 ...   (launcher test on gloo, tests/)
 """
 from __future__ import annotations
 
@@ -67,8 +69,9 @@ def parse():
     ap.add_argument("--batch", type=int, default=8, help="pairs per GPU (kitti_base.json train.batch_size)")
     ap.add_argument("--config", choices=sorted(CONFIGS), default="kitti")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-steps", type=int, default=6)
-    ap.add_argument("--cpu-batch", type=int, default=4)
+    ap.add_argument("--cpu-steps", type=int, default=3)
+    ap.add_argument("--cpu-batch", type=int, default=8,
+                    help="CPU baseline batch: the GPU's per-rank B=8 (BASELINE.md 3)")
     ap.add_argument("--no-replay", action="store_true",
                     help="skip the graph-replay device times (keeps a rocprofv3 run to real steps only)")
     ap.add_argument("--cudnn-benchmark", action="store_true",
@@ -76,6 +79,11 @@ def parse():
     ap.add_argument("--per-direction", action="store_true",
                     help="run with_bk as the reference's two batch-B passes instead of one batch-2B pass "
                          "(PWCLite.batch_directions = False)")
+    ap.add_argument("--device", choices=("cuda", "cpu"), default="cuda",
+                    help="cpu: launcher/plumbing test only (gloo, the cpu_baseline step with the oracle ops "
+                         "as the checker's stand-in; never a measurement)")
+    ap.add_argument("--hw", type=int, nargs=2, metavar=("H", "W"), default=None,
+                    help="frame size override (tests; the metric is KITTI 256x832)")
     ap.add_argument("--graph", action="store_true",
                     help="replay the step from HIP graphs (harness.GraphedTrainStep); measured equal to "
                          "eager at N=1 (the step is GPU-bound), so eager is the default")
@@ -95,18 +103,27 @@ def kernel_report(summary, device, steps, replay=True):
     from unsamflow_amd.kernel_timer import device_time_us, site_launcher, site_name
 
     rows, per_op = [], {}
-    best = None
+    best = best_dev = None
     for i, ((op, key), a) in enumerate(summary.items()):
         calls = a["n"] / max(1, steps)
         us = a["mean_us"]
         row = {
             "op": op, "shape": list(key), "site": site_name(op, key), "calls_per_step": calls,
-            "in_step_us": round(us, 2), "bytes": a["bytes"], "gbps": round(a["bytes"] / (us * 1e-6) / 1e9, 1),
-            "hbm_frac": round(a["bytes"] / (us * 1e-6) / 1e9 / HBM_PEAK_GBPS, 4),
-            "tflops": round(a["flops"] / (us * 1e-6) / 1e12, 2),
+            "in_step_us": round(us, 2), "bytes": a["bytes"],
+            "gbps_in_step": round(a["bytes"] / (us * 1e-6) / 1e9, 1),
+            "hbm_frac_in_step": round(a["bytes"] / (us * 1e-6) / 1e9 / HBM_PEAK_GBPS, 4),
         }
         if replay:
-            row["device_us"] = round(device_time_us(site_launcher(op, key, device, seed=i)), 2)
+            # the per-level HBM fraction uses the DEVICE time: at small sites the
+            # in-step interval also holds the GPU catching up with the host
+            # (2-4x rocprof at L0-L2, profiles/r01_v22_roofline_check.json)
+            dev_us = device_time_us(site_launcher(op, key, device, seed=i))
+            row["device_us"] = round(dev_us, 2)
+            row["gbps"] = round(a["bytes"] / (dev_us * 1e-6) / 1e9, 1)
+            row["hbm_frac"] = round(a["bytes"] / (dev_us * 1e-6) / 1e9 / HBM_PEAK_GBPS, 4)
+            row["tflops"] = round(a["flops"] / (dev_us * 1e-6) / 1e12, 2)
+            if best_dev is None or calls * dev_us > best_dev[0]:
+                best_dev = (calls * dev_us, row)
         rows.append(row)
         per_op[op] = per_op.get(op, 0.0) + calls * us
         if best is None or calls * us > best[0]:
@@ -117,10 +134,10 @@ def kernel_report(summary, device, steps, replay=True):
         "kernel": row["op"],
         "shape": row["shape"],
         "site": row["site"],
-        "achieved": row["gbps"],
+        "achieved": row["gbps_in_step"],
         "peak": HBM_PEAK_GBPS,
         "unit": "GB/s",
-        "frac": row["hbm_frac"],
+        "frac": row["hbm_frac_in_step"],
         "bytes_per_launch": row["bytes"],
         "mean_us": row["in_step_us"],
         "launches_timed": int(round(row["calls_per_step"] * steps)),
@@ -131,6 +148,13 @@ def kernel_report(summary, device, steps, replay=True):
     }
     if row["op"] == "warp_bwd" and row["shape"][5]:
         roof["atomic_floor"] = atomic_floor(row["shape"], row["in_step_us"])
+    if best_dev is not None:
+        # the dominant site by device time on synthetic inputs (smooth +-2 px
+        # flows): the model's own random-init flows are near zero, which
+        # flatters the warp backward's scatter in-step
+        d = best_dev[1]
+        roof["dominant_by_device"] = {"site": d["site"], "device_us": d["device_us"], "gbps": d["gbps"],
+                                      "frac": d["hbm_frac"], "us_per_step": round(best_dev[0], 1)}
     return rows, roof, {k: round(v, 1) for k, v in per_op.items()}
 
 
@@ -222,6 +246,32 @@ def survey_configs_cpu():
     return out
 
 
+KITTI_LEVELS = [(192, 4, 13), (128, 8, 26), (96, 16, 52), (64, 32, 104), (32, 64, 208)]
+
+
+def corr_levels_cpu(B=8):
+    """per-level KITTI correlation fwd / bwd (both grads) ms at
+    B=8 on the CPU oracle (correlation_native.py:13-23 restated, autograd bwd)."""
+    from oracle.corr import OracleCorrelation
+
+    corr = OracleCorrelation(4)
+    out = []
+    for C, H, W in KITTI_LEVELS:
+        g = torch.Generator().manual_seed(C)
+        x1 = torch.randn(B, C, H, W, generator=g, requires_grad=True)
+        x2 = torch.randn(B, C, H, W, generator=g, requires_grad=True)
+        go = torch.randn(B, 81, H, W, generator=g)
+        corr(x1, x2).backward(go)
+        x1.grad = x2.grad = None
+        t0 = time.perf_counter()
+        y = corr(x1, x2)
+        t1 = time.perf_counter()
+        y.backward(go)
+        t2 = time.perf_counter()
+        out.append({"shape": [B, C, H, W], "fwd_ms": round((t1 - t0) * 1e3, 2), "bwd_ms": round((t2 - t1) * 1e3, 2)})
+    return out
+
+
 def cpu_baseline(args, cfg_name):
     """Oracle (torch-CPU restatement) PWCLite step on the host cores, bounded."""
     from oracle.torch_ref import OracleCorrelation, oracle_flow_warp, oracle_occu_mask_backward
@@ -252,6 +302,7 @@ def cpu_baseline(args, cfg_name):
     return {
         "value": round(args.cpu_batch * args.cpu_steps / dt, 4),
         "survey_configs": configs,
+        "corr_levels": corr_levels_cpu(),
         "unit": "image-pairs/s",
         "cores": cores,
         "kind": "port",
@@ -261,34 +312,97 @@ def cpu_baseline(args, cfg_name):
     }
 
 
+def _free_port():
+    import socket
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def launch_ranks(n: int) -> int:
+    """--gpus N > 1 without a torch.distributed environment: start N rank
+    processes of this script (one per GPU, RANK = LOCAL_RANK = r, rendezvous on
+    127.0.0.1) and wait for them, as the reference's trainer spawns its own
+    world (train.py:228-234, mp.spawn(main_ddp, nprocs=world_size)). Called
+    before anything touches the GPU; the children are fresh processes (no exec
+    from this one). A rank that fails ends the others."""
+    import subprocess
+
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]], env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in live:
+                    q.terminate()
+        time.sleep(0.2)
+    return rc
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and rank == 0:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+    if world != args.gpus:
+        print(f"error: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        sys.exit(2)
     distributed = world > 1
-    torch.cuda.set_device(local_rank)
-    device = torch.device("cuda", local_rank)
+    on_gpu = args.device == "cuda"
+    if on_gpu:
+        torch.cuda.set_device(local_rank)
+        device = torch.device("cuda", local_rank)
+    else:
+        device = torch.device("cpu")
+        torch.set_num_threads(max(1, min(4, os.cpu_count() or 1)))
     if distributed:
-        dist.init_process_group("nccl", device_id=device)
+        if on_gpu:
+            dist.init_process_group("nccl", device_id=device)
+        else:
+            dist.init_process_group("gloo")
+        assert dist.get_world_size() == args.gpus, (dist.get_world_size(), args.gpus)
     torch.backends.cudnn.benchmark = bool(args.cudnn_benchmark)
 
-    from unsamflow_amd import _lib
     from unsamflow_amd.harness import GraphedTrainStep, TrainStep, broadcast_params, synthetic_pair
     from unsamflow_amd.kernel_timer import KernelTimer
 
-    _lib.load()  # fail loudly if the HIP library is missing
-    c = CONFIGS[args.config]
+    c = dict(CONFIGS[args.config])
+    if args.hw:
+        c["H"], c["W"] = args.hw
     cfg = cfg_for(args.config)
-    use_graph = args.graph
-    # graph mode: the whole step is captured once and replayed (harness.GraphedTrainStep);
-    # data parallel = one all-reduce of the flat gradient buffer between the two graphs
-    step = TrainStep(cfg, device, ddp=distributed and not use_graph, seed=42 + rank, capturable=use_graph)
+    if on_gpu:
+        from unsamflow_amd import _lib
+
+        _lib.load()  # fail loudly if the HIP library is missing
+        use_graph = args.graph
+        # graph mode: the whole step is captured once and replayed (harness.GraphedTrainStep);
+        # data parallel = one all-reduce of the flat gradient buffer between the two graphs
+        step = TrainStep(cfg, device, ddp=distributed and not use_graph, seed=42 + rank, capturable=use_graph)
+    else:
+        # launcher test only: the cpu_baseline step (oracle ops) under gloo DDP
+        from oracle.torch_ref import OracleCorrelation, oracle_flow_warp, oracle_occu_mask_backward
+
+        use_graph = False
+        step = TrainStep(cfg, device, ddp=distributed, seed=42, corr_module=OracleCorrelation(4),
+                         warp_fn=oracle_flow_warp, occ_backward_fn=oracle_occu_mask_backward, fused_adam=False)
     step.module.batch_directions = not args.per_direction
     img1, img2, s1, s2 = synthetic_pair(args.batch, c["H"], c["W"], device, seed=42 + rank,
                                         with_seg=args.config != "kitti")
+    sync = torch.cuda.synchronize if on_gpu else (lambda: None)
 
     if use_graph:
         if distributed:
@@ -301,19 +415,19 @@ def main():
         for i in range(args.warmup):
             step(img1, img2, s1, s2)
         run = lambda: step(img1, img2, s1, s2)  # noqa: E731
-    torch.cuda.synchronize()
+    sync()
 
     if distributed:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     # eager: two event records per hot-path launch inside the timed region (no syncs);
     # graph replays carry no host code, so their per-site times come from the
     # in-step pass below
-    with KernelTimer(enabled=not use_graph) as kt:
+    with KernelTimer(enabled=on_gpu and not use_graph) as kt:
         t0 = time.perf_counter()
         for _ in range(args.steps):
             loss = run()
-        torch.cuda.synchronize()
+        sync()
     if distributed:
         dist.barrier()
     elapsed = time.perf_counter() - t0
@@ -321,28 +435,30 @@ def main():
         # per-site kernel times: the same step run eagerly for K steps with HIP
         # events around every library launch (kernel durations do not depend on
         # how the launch was issued; rocprofv3 of the replays cross-checks them)
-        torch.cuda.synchronize()
+        sync()
         with KernelTimer() as kt:
             for _ in range(args.steps):
                 step(img1, img2, s1, s2)
-            torch.cuda.synchronize()
+            sync()
     if distributed:
         t = torch.tensor([elapsed], device=device, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
     loss_val = float(loss.item())
 
-    summary = kt.summary()
-    rows, roof, per_op_us = kernel_report(summary, device, args.steps, replay=not args.no_replay)
-    roof["copy_ceiling_gbps"] = copy_ceiling_gbps(device)
-    roof["frac_of_copy"] = round(roof["achieved"] / roof["copy_ceiling_gbps"], 4)
-    traffic, src = pmc_traffic(roof["kernel"], roof["shape"])
-    roof["traffic"] = traffic
-    roof["traffic_source"] = src
-    gpu_configs = None if args.no_replay else survey_configs_gpu(device)
+    rows = roof = per_op_us = gpu_configs = None
+    if on_gpu:
+        summary = kt.summary()
+        rows, roof, per_op_us = kernel_report(summary, device, args.steps, replay=not args.no_replay)
+        roof["copy_ceiling_gbps"] = copy_ceiling_gbps(device)
+        roof["frac_of_copy"] = round(roof["achieved"] / roof["copy_ceiling_gbps"], 4)
+        traffic, src = pmc_traffic(roof["kernel"], roof["shape"])
+        roof["traffic"] = traffic
+        roof["traffic_source"] = src
+        gpu_configs = None if args.no_replay else survey_configs_gpu(device)
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if on_gpu and rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args, args.config)
 
     if rank == 0:
@@ -378,6 +494,8 @@ def main():
             "levels": rows,
             "final_loss": round(loss_val, 6),
         }
+        if not on_gpu:
+            out["device"] = "cpu (launcher test: oracle ops, not a measurement)"
         print(json.dumps(out), flush=True)
     if distributed:
         dist.destroy_process_group()

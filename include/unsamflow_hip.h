@@ -24,6 +24,8 @@
  *                        scatter_add_ of bilinear weights)
  *   usf_occ_backward_f32 <- get_occu_mask_backward (warp_utils.py:120-126),
  *                        caller losses/flow_loss.py:101-103 (occ_from_back)
+ *   usf_occ_bidirection_f32 <- get_occu_mask_bidirection (warp_utils.py:109-117),
+ *                        caller losses/flow_loss.py:104-107 (occ_from_back = false)
  *   usf_photo_loss_*  <- the per-scale warp + loss_photomatric composition of
  *                        losses/flow_loss.py:127-148
  *   usf_area_pyramid  <- the loss's per-scale F.interpolate(im, mode="area")
@@ -62,7 +64,7 @@
 extern "C" {
 #endif
 
-#define USF_ABI_VERSION 3
+#define USF_ABI_VERSION 4
 #define USF_EINVAL (-1)
 
 /* padding modes for the warp (flow_warp `pad` argument) */
@@ -172,6 +174,16 @@ int usf_splat_map_f32(const float* flow, long long flow_bstride, float* map,
  * occ: [B,1,H,W] dense, overwritten. */
 int usf_occ_backward_f32(const float* flow21, long long flow_bstride, float* occ,
                          int B, int H, int W, float th, void* stream);
+
+/* Forward-backward consistency occlusion mask (get_occu_mask_bidirection,
+ * utils/warp_utils.py:109-117; stage-1 configs, occ_from_back = false), fused:
+ *   w21 = flow_warp(flow21, flow12, pad="zeros"); d = flow12 + w21
+ *   occ = |d|^2 > scale * (|flow12|^2 + |w21|^2) + bias ? 1 : 0
+ * flow12, flow21: [B,2,H,W] with batch strides (channel slices allowed);
+ * occ: [B,1,H,W] dense, overwritten. Each sum/product rounded as torch does. */
+int usf_occ_bidirection_f32(const float* flow12, long long flow12_bstride, const float* flow21,
+                            long long flow21_bstride, float* occ, int B, int H, int W,
+                            float scale, float bias, void* stream);
 
 /* Fused occlusion-aware photometric loss of one scale and direction
  * (losses/flow_loss.py:127-148, loss_photomatric :33-50, SSIM

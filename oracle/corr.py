@@ -57,6 +57,22 @@ def corr_backward_np(x1: np.ndarray, x2: np.ndarray, g: np.ndarray, d: int = 4, 
     return gx1, gx2p[:, :, d:d + H, d:d + W]
 
 
+def corr_backward_torch64(x1: torch.Tensor, x2: torch.Tensor, g: torch.Tensor, d: int = 4):
+    """corr_backward_np in torch-CPU float64 (same formulas, multi-threaded): the
+    checker for full-size shapes, e.g. the decoder's L4 site at batch 16."""
+    B, C, H, W = x1.shape
+    a = x1.double()
+    x2p = F.pad(x2.double(), [d] * 4)
+    gg = g.double() / C
+    gx1 = torch.zeros((B, C, H, W), dtype=torch.float64)
+    gx2p = torch.zeros_like(x2p)
+    for k, i, j in _shifts(d):
+        gk = gg[:, k:k + 1]
+        gx1 += gk * x2p[:, :, i:i + H, j:j + W]
+        gx2p[:, :, i:i + H, j:j + W] += gk * a
+    return gx1, gx2p[:, :, d:d + H, d:d + W]
+
+
 def corr_forward_torch(x1: torch.Tensor, x2: torch.Tensor, d: int = 4) -> torch.Tensor:
     """torch-CPU restatement of correlation_native.py:13-23 (differentiable by autograd)."""
     B, C, H, W = x1.shape

@@ -115,6 +115,33 @@ def warp_backward_np(x: np.ndarray, flow: np.ndarray, gout: np.ndarray, pad: str
     return gx, gflow
 
 
+def occu_mask_bidirection_np(flow12: np.ndarray, flow21: np.ndarray, scale: float = 0.01, bias: float = 0.5,
+                             warped: np.ndarray | None = None) -> np.ndarray:
+    """get_occu_mask_bidirection (utils/warp_utils.py:109-117) in float32 numpy:
+    ``w = flow_warp(flow21, flow12, pad="zeros")`` (or ``warped``, e.g. the
+    reference's own warp output from a golden capture), ``d = flow12 + w``,
+    occluded where ``|d|^2 > scale * (|flow12|^2 + |w|^2) + bias``; each
+    channel sum over the 2 components is ``a + b`` as torch's ``sum(1)``, the
+    Python scalars act as float32 (torch's wrapped-number promotion)."""
+    f = flow12.astype(f32)
+    w = warp_forward_np(flow21, flow12, "zeros") if warped is None else warped.astype(f32)
+    d = f + w
+    mag = (f[:, 0] * f[:, 0] + f[:, 1] * f[:, 1]) + (w[:, 0] * w[:, 0] + w[:, 1] * w[:, 1])
+    th = f32(scale) * mag + f32(bias)
+    return ((d[:, 0] * d[:, 0] + d[:, 1] * d[:, 1]) > th)[:, None].astype(f32)
+
+
+def occu_bidirection_margin(flow12: np.ndarray, flow21: np.ndarray, scale: float = 0.01,
+                            bias: float = 0.5) -> np.ndarray:
+    """|  |d|^2 - threshold  | per pixel (float64): where the mask decision is
+    within rounding of the threshold, two correct implementations may differ."""
+    f = flow12.astype(np.float64)
+    w = warp_forward_np(flow21, flow12, "zeros").astype(np.float64)
+    d = f + w
+    th = scale * ((f ** 2).sum(1) + (w ** 2).sum(1)) + bias
+    return np.abs((d ** 2).sum(1) - th)[:, None]
+
+
 def warp_bytes(B: int, C: int, H: int, W: int, backward: bool = False, need_x: bool = True) -> int:
     """Algorithmic HBM bytes."""
     if not backward:

@@ -34,6 +34,7 @@ def test_header_declares_the_abi():
          "usf_corr_fwd_ex_f32", "usf_corr_fwd_workspace", "usf_corr_bwd_ex_f32", "usf_corr_act_mask_words",
          "usf_corr_bwd_ex_scratch",
          "usf_warp_fwd_f32", "usf_warp_bwd_f32", "usf_splat_map_f32", "usf_occ_backward_f32",
+         "usf_occ_bidirection_f32",
          "usf_photo_loss_partials", "usf_photo_loss_fwd_f32", "usf_photo_loss_pair_fwd_f32",
          "usf_photo_loss_bwd_f32",
          "usf_flow_upsample_f32", "usf_flow_upsample_bwd_f32", "usf_area_pyramid_f32",
@@ -57,7 +58,7 @@ def test_library_exports_every_declared_symbol(lib):
 def test_abi_version(lib):
     from unsamflow_amd import _lib
 
-    assert lib.usf_abi_version() == _lib.ABI_VERSION == 3
+    assert lib.usf_abi_version() == _lib.ABI_VERSION == 4
 
 
 def test_no_torch_types_in_abi():

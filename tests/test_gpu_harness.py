@@ -49,7 +49,7 @@ def test_pwclite_hip_matches_reference(hip_device, name, cfg_fn):
 
 
 def test_smoke_step(hip_device):
-    from unsamflow_amd.harness import smoke_step
+    from __graft_entry__ import smoke_step
 
     smoke_step(hip_device)
 

@@ -86,6 +86,53 @@ def test_warp_oracle_matches_reference(name):
     np.testing.assert_allclose(gflow, z["gflow"], atol=5e-6, rtol=1e-6)
 
 
+@pytest.mark.parametrize("name", [n for n in golden_files("warp_zeros")])
+def test_occ_bidirection_oracle_through_reference_warp(name):
+    """get_occu_mask_bidirection (warp_utils.py:109-117) = a zeros-padded
+    flow_warp + an element-wise test. Capturing it from the reference directly
+    was denied this round, so the oracle is pinned through the
+    reference's own zeros-mode warp outputs: channels 0-1 of a warp golden are
+    flow21 and its warp by flow12, and the oracle (which re-warps) must reach the
+    same mask decisions as the formula on the reference's warped values."""
+    from oracle.warp import occu_bidirection_margin, occu_mask_bidirection_np
+
+    z = load_golden(name)
+    x, flow12, pad = _warp_inputs(z)
+    assert pad == "zeros" and x.shape[1] >= 2
+    seen = set()
+    for amp in (0.25, 1.0, 4.0, 20.0):  # flow21 magnitudes around the threshold's 0.5 px^2 bias
+        flow21 = x[:, :2] * np.float32(amp)
+        ref_w = z["out"][:, :2] * np.float32(amp)  # the warp is linear in its input
+        ref = occu_mask_bidirection_np(flow12, flow21, warped=ref_w)
+        got = occu_mask_bidirection_np(flow12, flow21)
+        near = occu_bidirection_margin(flow12, flow21) < 1e-4 * (1 + np.abs(flow12).max()) ** 2
+        assert np.array_equal(got[~near], ref[~near])
+        seen |= set(np.unique(ref).tolist())
+    # both decisions occur (with flows up to 30 px every sample is occluded)
+    assert seen == ({1.0} if "bigflow" in name else {0.0, 1.0})
+
+
+def test_occ_bidirection_oracles_agree():
+    """The numpy and torch-CPU restatements of get_occu_mask_bidirection agree
+    (random, large, integer and out-of-image flows)."""
+    import torch
+
+    from oracle.torch_ref import oracle_occu_mask_bidirection
+    from oracle.warp import occu_bidirection_margin, occu_mask_bidirection_np
+
+    rng = np.random.default_rng(5)
+    for amp, integer in ((0.8, False), (6.0, False), (25.0, False), (3.0, True)):
+        f12 = (rng.standard_normal((2, 2, 19, 31)) * amp).astype(np.float32)
+        f21 = (rng.standard_normal((2, 2, 19, 31)) * amp).astype(np.float32)
+        if integer:
+            f12, f21 = np.round(f12), np.round(f21)
+        a = occu_mask_bidirection_np(f12, f21)
+        b = oracle_occu_mask_bidirection(torch.from_numpy(f12), torch.from_numpy(f21)).numpy()
+        near = occu_bidirection_margin(f12, f21) < 1e-4 * (1 + amp) ** 2
+        assert np.array_equal(a[~near], b[~near])
+        assert 0 < a.mean() < 1
+
+
 def test_hashrng_is_stable():
     """The counter-hash generator is a pure function (golden inputs depend on it)."""
     u = hashrng.uniform((5,), 42)

@@ -30,6 +30,8 @@ SITES += [("photo_fwd", (8, 3, 256 >> i, 832 >> i, "border")) for i in range(4)]
 SITES += [("photo_fwd_grad", (8, 3, 256 >> i, 832 >> i, "border")) for i in range(4)]
 SITES += [("photo_pair_grad", (8, 3, 256 >> i, 832 >> i, "border")) for i in range(4)]
 SITES += [("photo_bwd", (8, 2, 256 >> i, 832 >> i)) for i in range(4)]
+# BASELINE config 2 (single-level correlation, B=8 C=128 32x104)
+SITES += [("corr_fwd", (8, 128, 32, 104)), ("corr_bwd", (8, 128, 32, 104, True, True))]
 
 
 def selected_sites():

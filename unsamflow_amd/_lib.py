@@ -17,7 +17,7 @@ from pathlib import Path
 import torch  # noqa: F401  (load torch's HIP runtime before the plugin)
 
 _LIB_PATH = Path(os.environ.get("USF_LIB", Path(__file__).resolve().parent / "lib" / "libunsamflow_hip.so"))
-ABI_VERSION = 3
+ABI_VERSION = 4
 PAD_ZEROS = 0
 PAD_BORDER = 1
 
@@ -64,6 +64,11 @@ _SIGNATURES = {
     ),
     "usf_occ_backward_f32": (
         [_c_float_p, ctypes.c_longlong, _c_float_p] + [ctypes.c_int] * 3 + [ctypes.c_float, ctypes.c_void_p],
+        ctypes.c_int,
+    ),
+    "usf_occ_bidirection_f32": (
+        [_c_float_p, ctypes.c_longlong, _c_float_p, ctypes.c_longlong, _c_float_p] + [ctypes.c_int] * 3
+        + [ctypes.c_float, ctypes.c_float, ctypes.c_void_p],
         ctypes.c_int,
     ),
     "usf_photo_loss_partials": ([ctypes.c_int] * 3, ctypes.c_int),

@@ -42,15 +42,19 @@ class CorrLeakyCatFunction(Function):
             off += e.shape[1]
         ctx.md, ctx.slope, ctx.n_pairs, ctx.k2 = max_displacement, slope, n_pairs, K2
         ctx.extra_ch = [e.shape[1] for e in extras]
-        ctx.has_mask = masks[0] is not None
-        ctx.save_for_backward(*[t for p in pairs for t in p], *(masks if ctx.has_mask else []), buf)
+        # per pair: with add_mask_corr the pairs can differ in C, so one pair's
+        # forward may split its channel loop (no mask) while the other's writes one
+        ctx.mask_idx = [i for i, m in enumerate(masks) if m is not None]
+        ctx.save_for_backward(*[t for p in pairs for t in p], *[masks[i] for i in ctx.mask_idx], buf)
         return buf
 
     @staticmethod
     def backward(ctx, gbuf):
         saved = ctx.saved_tensors
         buf = saved[-1]
-        masks = saved[2 * ctx.n_pairs:2 * ctx.n_pairs + ctx.n_pairs] if ctx.has_mask else [None] * ctx.n_pairs
+        masks = [None] * ctx.n_pairs
+        for j, i in enumerate(ctx.mask_idx):
+            masks[i] = saved[2 * ctx.n_pairs + j]
         grads = []
         off = 0
         gbuf = gbuf if gbuf.is_contiguous() else gbuf.contiguous()

@@ -302,6 +302,20 @@ int usf_occ_backward_f32(const float* flow21, long long flow_bstride, float* occ
                 (hipStream_t)stream);
 }
 
+int usf_occ_bidirection_f32(const float* flow12, long long flow12_bstride, const float* flow21,
+                            long long flow21_bstride, float* occ, int B, int H, int W, float scale,
+                            float bias, void* stream) {
+  clear_error();
+  if (!check_splat("usf_occ_bidirection_f32", flow12, flow12_bstride, occ, B, H, W) ||
+      !check_splat("usf_occ_bidirection_f32", flow21, flow21_bstride, occ, B, H, W))
+    return USF_EINVAL;
+  if (const int pe = pre_check("usf_occ_bidirection_f32", (hipStream_t)stream)) return pe;
+  return finish("usf_occ_bidirection_f32",
+                occ_bidirection_launch(flow12, flow12_bstride, flow21, flow21_bstride, occ, B, H, W, scale,
+                                       bias, (hipStream_t)stream),
+                (hipStream_t)stream);
+}
+
 int usf_photo_loss_partials(int B, int H, int W) {
   return (B > 0 && H > 0 && W > 0) ? photo_partials(B, H, W) : 0;
 }

@@ -706,7 +706,8 @@ __device__ __forceinline__ void corr_bwd_tile(float* sm, const float* __restrict
   // load is clamped into the row and the lanes at the image edge pick their
   // elements out of it by index.
   float gv[DYW][K][PX];
-  static_assert(!AM || (PX == 4 && K <= 16), "sign-mask derivative: 4-pixel runs (xb % 4 == 0)");
+  // the mask words cover pixels xb - 4 .. xb + 7 (mw[0..2]), i.e. ei in [-d, 3 + d] for d <= 4
+  static_assert(!AM || (PX == 4 && D <= 4), "sign-mask derivative: 4-pixel runs, d <= 4");
 #pragma unroll
   for (int t = 0; t < DYW; ++t) {
     const int dy = wave * DYW + t;

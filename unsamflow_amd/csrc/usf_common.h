@@ -100,6 +100,8 @@ hipError_t splat_launch(const float* flow, long long flow_bstride, float* map, i
                         bool absolute, hipStream_t s);
 hipError_t occ_backward_launch(const float* flow, long long flow_bstride, float* occ, int B, int H,
                                int W, float th, hipStream_t s);
+hipError_t occ_bidirection_launch(const float* flow12, long long bs12, const float* flow21, long long bs21,
+                                  float* occ, int B, int H, int W, float scale, float bias, hipStream_t s);
 
 int photo_partials(int B, int H, int W);
 hipError_t photo_fwd_launch(const float* src, const float* tgt, const float* mask, const float* flow,

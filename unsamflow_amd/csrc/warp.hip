@@ -972,4 +972,52 @@ hipError_t occ_backward_launch(const float* flow, long long fbs, float* occ, int
   return hipGetLastError();
 }
 
+namespace {
+// Forward-backward consistency occlusion (get_occu_mask_bidirection,
+// warp_utils.py:109-117), one thread per pixel:
+//   w21  = flow_warp(flow21, flow12, pad="zeros")            (:110)
+//   diff = flow12 + w21                                        (:111)
+//   mag  = (f12_u^2 + f12_v^2) + (w21_u^2 + w21_v^2)           (:112-114)
+//   occ  = (diff_u^2 + diff_v^2) > 0.01 * mag + 0.5 ? 1 : 0    (:115-117)
+// Each product and sum is rounded separately, as torch evaluates them (the
+// channel sums over 2 elements are a + b), so the mask decision is the
+// reference's bit for bit where the warp is.
+__global__ __launch_bounds__(256) void occ_bidir_kernel(const float* __restrict__ f12, long long bs12,
+                                                        const float* __restrict__ f21, long long bs21,
+                                                        float* __restrict__ occ, int H, int W,
+                                                        float scale, float bias) {
+#pragma clang fp contract(off)
+  const int HW = H * W;
+  const int p = blockIdx.x * 256 + threadIdx.x;
+  const int b = blockIdx.y;
+  if (p >= HW) return;
+  const int y = p / W, x = p - y * W;
+  const float* a = f12 + b * bs12;
+  const float* c = f21 + b * bs21;
+  const float u = a[p], v = a[HW + p];
+  const Tap t = make_tap(u, v, x, y, H, W, false);
+  const float wnw = t.s * t.e, wne = t.s * t.w, wsw = t.n * t.e, wse = t.n * t.w;
+  float w[2];
+#pragma unroll
+  for (int ch = 0; ch < 2; ++ch) {
+    const float* cc = c + ch * HW;
+    const float vnw = t.m_nw ? cc[t.o_nw] : 0.f, vne = t.m_ne ? cc[t.o_ne] : 0.f;
+    const float vsw = t.m_sw ? cc[t.o_sw] : 0.f, vse = t.m_se ? cc[t.o_se] : 0.f;
+    w[ch] = vnw * wnw + vne * wne + vsw * wsw + vse * wse;
+  }
+  const float du = u + w[0], dv = v + w[1];
+  const float mag = (u * u + v * v) + (w[0] * w[0] + w[1] * w[1]);
+  const float th = scale * mag + bias;
+  occ[(size_t)b * HW + p] = (du * du + dv * dv) > th ? 1.f : 0.f;
+}
+}  // namespace
+
+hipError_t occ_bidirection_launch(const float* flow12, long long bs12, const float* flow21, long long bs21,
+                                  float* occ, int B, int H, int W, float scale, float bias, hipStream_t s) {
+  const int HW = H * W;
+  hipLaunchKernelGGL(occ_bidir_kernel, dim3((unsigned)((HW + 255) / 256), (unsigned)B), dim3(256), 0, s,
+                     flow12, bs12, flow21, bs21, occ, H, W, scale, bias);
+  return hipGetLastError();
+}
+
 }  // namespace usf

@@ -225,32 +225,3 @@ class GraphedTrainStep:
         self.step.scheduler.step()
         return self.loss
 
-
-def smoke_step(device) -> None:
-    """Tiny PWCLite step on ``device`` checked against the same model on CPU with
-    the oracle ops (hash-initialised weights, 64x128, B=1)."""
-    from oracle.hashrng import hash_init_, uniform
-    from oracle.torch_ref import OracleCorrelation, oracle_flow_warp, oracle_occu_mask_backward
-
-    from .config import kitti_base
-
-    cfg = kitti_base()
-    gpu = TrainStep(cfg, device)
-    cpu = TrainStep(kitti_base(), "cpu", corr_module=OracleCorrelation(4), warp_fn=oracle_flow_warp,
-                    occ_backward_fn=oracle_occu_mask_backward)
-    hash_init_(gpu.module, seed=1)
-    hash_init_(cpu.module, seed=1)
-    im1 = torch.from_numpy(uniform((1, 3, 64, 128), 11))
-    im2 = torch.from_numpy(uniform((1, 3, 64, 128), 12))
-    lg, fg = gpu.forward_loss(im1.to(device), im2.to(device))
-    lc, fc = cpu.forward_loss(im1, im2)
-    lg.backward()
-    lc.backward()
-    torch.cuda.synchronize(device)
-    assert torch.isfinite(lg), lg
-    assert abs(lg.item() - lc.item()) <= 1e-4 * abs(lc.item()) + 1e-6, (lg.item(), lc.item())
-    torch.testing.assert_close(fg[0].cpu(), fc[0].detach(), atol=2e-4, rtol=1e-3)
-    for (n, pg), pc in zip(gpu.module.named_parameters(), cpu.module.parameters()):
-        torch.testing.assert_close(pg.grad.cpu(), pc.grad, atol=1e-4, rtol=5e-3, msg=n)
-    step = gpu(im1.to(device), im2.to(device))
-    assert torch.isfinite(step)

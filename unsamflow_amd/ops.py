@@ -242,6 +242,23 @@ def occ_backward(flow21: torch.Tensor, th: float = 0.2) -> torch.Tensor:
     return out
 
 
+def occ_bidirection(flow12: torch.Tensor, flow21: torch.Tensor, scale: float = 0.01, bias: float = 0.5
+                    ) -> torch.Tensor:
+    """Occlusion mask get_occu_mask_bidirection (warp_utils.py:109-117) -> [B,1,H,W] float, one kernel."""
+    f1, bs1, B, H, W = _flow_arg(flow12, "flow12")
+    f2, bs2, B2, H2, W2 = _flow_arg(flow21, "flow21")
+    if (B2, H2, W2) != (B, H, W):
+        raise ValueError(f"flow21 shape {tuple(flow21.shape)} != flow12 shape {tuple(flow12.shape)}")
+    out = torch.empty((B, 1, H, W), device=flow12.device, dtype=torch.float32)
+    lib = _lib.load()
+    with torch.cuda.device(flow12.device), _kt.timed("occ_bidir", (B, 1, H, W), flow12.device,
+                                                       4 * B * H * W * 5):
+        rc = lib.usf_occ_bidirection_f32(f1.data_ptr(), bs1, f2.data_ptr(), bs2, out.data_ptr(), B, H, W,
+                                         float(scale), float(bias), _lib.stream_handle(flow12.device))
+    _lib.check(rc, "usf_occ_bidirection_f32")
+    return out
+
+
 def _photo_args(src, tgt, mask, flow):
     for n, t in (("src", src), ("tgt", tgt), ("mask", mask)):
         _require_device_f32(n, t)

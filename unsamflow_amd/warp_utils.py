@@ -80,10 +80,8 @@ def get_occu_mask_backward(flow21: torch.Tensor, th: float = 0.2) -> torch.Tenso
 
 def get_occu_mask_bidirection(flow12: torch.Tensor, flow21: torch.Tensor, scale: float = 0.01,
                               bias: float = 0.5) -> torch.Tensor:
-    """Forward-backward consistency occlusion mask (:109-117)."""
-    flow21_warped = flow_warp(flow21, flow12, pad="zeros")
-    flow12_diff = flow12 + flow21_warped
-    mag = (flow12 * flow12).sum(1, keepdim=True) + (flow21_warped * flow21_warped).sum(1, keepdim=True)
-    occ_thresh = scale * mag + bias
-    occ = (flow12_diff * flow12_diff).sum(1, keepdim=True) > occ_thresh
-    return occ.float()
+    """Forward-backward consistency occlusion mask (:109-117): the zeros-padded
+    warp of flow21 by flow12, the consistency test and the threshold in one
+    kernel (usf_occ_bidirection_f32). No gradient flows through it (the
+    reference's comparison has none either)."""
+    return ops.occ_bidirection(flow12.detach(), flow21.detach(), scale, bias)
