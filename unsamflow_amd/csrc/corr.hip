@@ -645,6 +645,9 @@ struct BwdCfg {
   static constexpr int XIMG = X::N;
   static constexpr int RED = NW * CC * TH * TW;      // per-wave partial sums
   // <4,4,8,3,4>: 40 KB, so four workgroups fit the 160 KB LDS of a CU
+  // two x image buffers: the DMA of stage s + 1 is in flight during stage s.
+  // A third buffer (two stages in flight, 48 KB: 3 workgroups per CU) was
+  // slower: L4 76.2 vs 67.8 us (profiles/ab_r02/bwd_nbuf.json)
   static constexpr int LDSN = 2 * XIMG + RED;
   static_assert(PX % 4 == 0, "PX must be a multiple of 4");
   static_assert(V == 1 || L::X4, "16-byte DMA needs the 4-aligned layout");
@@ -658,35 +661,30 @@ __device__ __forceinline__ unsigned long long buf_load8(__amdgpu_buffer_rsrc_t r
   return (unsigned long long)v.x | ((unsigned long long)v.y << 32);
 }
 
-template <int D, int PX, int SEGX, int NW, int CC, int V, bool G2, bool AM>
-__device__ __forceinline__ void corr_bwd_tile(float* sm, const float* __restrict__ xs,
-                                              const float* __restrict__ g,
-                                              float* __restrict__ gx, int tile, int group, int b,
-                                              int C, int H, int W, int tiles_x, int cg,
-                                              const BwdEpi& ep) {
-  using F = BwdCfg<D, PX, SEGX, NW, CC, V>;
-  constexpr int K = F::K, TW = F::TW, TH = F::TH, NT = F::NT, S = F::S, P = F::P;
-  constexpr int WIN = F::WIN, DYW = F::DYW, XIMG = F::XIMG;
-  constexpr bool B64 = F::L::B64;
-  float* red = sm + 2 * XIMG;
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int cbeg = group * cg;
-  const int cend = min(C, cbeg + cg);
-  const int ty = tile / tiles_x;
-  const int tx = tile - ty * tiles_x;
-  const int y0 = ty * TH, x0 = tx * TW;
-  const int r = F::L::row(lane), q = F::L::seg(lane);
-  const int y = y0 + r;
-  const int xb = x0 + q * PX;
-
+// Occupancy target of the backward kernels (see corr_bwd_kernel).
+#ifndef USF_BWD_WAVES_PER_EU
+#define USF_BWD_WAVES_PER_EU 3
+#endif
+// Work items per XCD chunk of the backward's block order (see corr_bwd_kernel).
+#ifndef USF_BWD_CHUNK
+#define USF_BWD_CHUNK 14
+#endif
+// g prologue of one wave: its DYW displacement rows of g for its PX pixels,
+// read once per workgroup. gx1 (G2 == false) takes g at the lane's own pixels;
+// gx2 (G2 == true) takes, for displacement k, g at pixel - delta_k. All loads
+// are unconditional at clamped in-bounds offsets (no branch, so no wait, inside
+// the burst). With W % 4 == 0 (V == 4) each 4-pixel run is ONE 16-byte load:
+// the dword form made every wave-instruction touch 8 cache lines for 32 of
+// their 128 bytes, 4 times over. gx2's runs start at xb - dx + d (dword
+// aligned): the load is clamped into the row and the lanes at the image edge
+// pick their elements out of it by index. AM: the LeakyReLU derivative from
+// the forward's sign mask, applied inside the loads.
+template <int D, int PX, int SEGX, int NW, int CC, int V, bool G2, bool AM, int DYW, int K>
+__device__ __forceinline__ void bwd_load_g(float (&gv)[DYW][K][PX], const float* __restrict__ gb,
+                                           const BwdEpi& ep, int b, int wave, int y, int xb, int H,
+                                           int W) {
+  static_assert(DYW == BwdCfg<D, PX, SEGX, NW, CC, V>::DYW && K == 2 * D + 1, "g slice shape");
   const int HW = H * W;
-  const float* xsb = xs + (size_t)b * C * HW;
-  // g of sample b at b * ep.g_bstride: a channel slice of the concat gradient,
-  // or the dense [B,K*K,H,W] tensor
-  const float* gb = g + (size_t)b * ep.g_bstride;
   // raw buffer descriptors over this sample's K*K planes: 16-byte loads with a
   // 32-bit offset (one VGPR per address instead of a 64-bit pointer pair)
   const auto grs = plane_buf(gb, K * K * HW * 4);
@@ -696,16 +694,6 @@ __device__ __forceinline__ void corr_bwd_tile(float* sm, const float* __restrict
                             const_cast<unsigned long long*>(ep.mask + (size_t)b * K * H * W4), 0,
                             K * H * W4 * 8, kRsrcFlags)
                       : grs;
-
-  // this wave's DYW rows of g for its PX pixels, read once. All loads are
-  // unconditional at clamped in-bounds offsets (no branch, so no wait, inside
-  // the burst). With W % 4 == 0 (V == 4) each 4-pixel run is ONE 16-byte load:
-  // the dword form made every wave-instruction touch 8 cache lines for 32 of
-  // their 128 bytes, 4 times over (PMC: the backward is bound by its L2 request
-  // volume). gx2's runs start at xb - dx + d (dword aligned): the
-  // load is clamped into the row and the lanes at the image edge pick their
-  // elements out of it by index.
-  float gv[DYW][K][PX];
   // the mask words cover pixels xb - 4 .. xb + 7 (mw[0..2]), i.e. ei in [-d, 3 + d] for d <= 4
   static_assert(!AM || (PX == 4 && D <= 4), "sign-mask derivative: 4-pixel runs, d <= 4");
 #pragma unroll
@@ -772,17 +760,166 @@ __device__ __forceinline__ void corr_bwd_tile(float* sm, const float* __restrict
       }
     }
   }
+}
+
+// One stage of CC channels for one wave: its DYW displacement rows summed in
+// registers per channel, the partial written lane-linear (lane*PX:
+// conflict-free ds_write_b128) to rp + c * TH * TW.
+template <int D, int PX, int SEGX, int NW, int CC, int V, bool G2, int DYW, int K>
+__device__ __forceinline__ void bwd_stage(const float (&gv)[DYW][K][PX], const float* cur, float* rp,
+                                          int wave, int r, int q, const BwdEpi& ep) {
+  using F = BwdCfg<D, PX, SEGX, NW, CC, V>;
+  constexpr int TW = F::TW, TH = F::TH, S = F::S, P = F::P;
+  constexpr int WIN = F::WIN;
+  constexpr bool B64 = F::L::B64;
+#pragma unroll 2
+  for (int c = 0; c < CC; ++c) {
+    float acc[PX];
+#pragma unroll
+    for (int i = 0; i < PX; ++i) acc[i] = 0.f;
+#pragma unroll
+    for (int t = 0; t < DYW; ++t) {
+      const int dy = wave * DYW + t;
+      // compile-time true when the waves' rows tile K exactly (NW * DYW == K):
+      // no per-row branch, so the compiler overlaps one row's ds_reads with the
+      // previous row's FMAs (L4 75.4 -> 70.6 us, profiles/ab_r02)
+#if defined(USF_BWD_PROBE) && USF_BWD_PROBE == 5
+      if (ep.slope == 12345.f) {  // probe: no FMAs (timing only)
+#else
+      if (NW * DYW == K || dy < K) {
+#endif
+        const int rs = G2 ? (2 * D - dy) : dy;
+        float w[WIN];
+        lds_read<B64>(cur + c * P + (r + rs) * S + q * PX, w);
+#pragma unroll
+        for (int dx = 0; dx < K; ++dx) {
+          const int cs = G2 ? (2 * D - dx) : dx;
+#pragma unroll
+          for (int i = 0; i < PX; ++i) acc[i] = fmaf(gv[t][dx][i], w[i + cs], acc[i]);
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < PX / 4; ++i)
+      reinterpret_cast<float4*>(rp + c * (TH * TW))[i] =
+          make_float4(acc[4 * i], acc[4 * i + 1], acc[4 * i + 2], acc[4 * i + 3]);
+  }
+}
+
+#ifndef USF_BWD_RCP
+#define USF_BWD_RCP 1
+#endif
+// Combine the NW wave partials of one direction (red: [NW][CC][TH*TW]) in a
+// fixed order, 4 pixels per thread (a lane's PX pixels are contiguous in its
+// partial slot), and write channels [c0, c0 + CC) of the tile, divided by C.
+template <int D, int PX, int SEGX, int NW, int CC, int V>
+__device__ __forceinline__ void bwd_combine(const float* red, float* gxb, int t1, int nthr, int c0,
+                                            int cend, int y0, int x0, int H, int W, float cf) {
+  using F = BwdCfg<D, PX, SEGX, NW, CC, V>;
+  constexpr int TW = F::TW, TH = F::TH;
+  const int HW = H * W;
+  const bool vec_out = (W & 3) == 0;
+  for (int o = t1; o < CC * TH * TW / 4; o += nthr) {
+    const int c = o / (TH * TW / 4);
+    const int pix = (o - c * (TH * TW / 4)) * 4;
+    const int py = pix / TW, pxo = pix % TW;
+    // lane that owns pixel (py, pxo) under the layout's lane mapping
+    const int ol = F::L::COLMAJOR ? (pxo / PX) * TH + py : py * SEGX + pxo / PX;
+    const int ridx = c * (TH * TW) + ol * PX + pxo % PX;
+    float4 sum = *reinterpret_cast<const float4*>(red + ridx);
+#pragma unroll
+    for (int w2 = 1; w2 < NW; ++w2) {
+      const float4 v = *reinterpret_cast<const float4*>(red + w2 * (CC * TH * TW) + ridx);
+      sum.x += v.x; sum.y += v.y; sum.z += v.z; sum.w += v.w;
+    }
+    const int yy = y0 + py, xx = x0 + pxo;
+    if (c0 + c < cend && yy < H) {
+      float* o4 = gxb + (size_t)(c0 + c) * HW + yy * W + xx;
+#if USF_BWD_RCP
+      // the channel mean as a multiply by 1/C (exact for power-of-two C, else
+      // within 1 ulp of the division): an IEEE division is ~10 VALU
+      // instructions, 4 per quad (profiles/ab_r02)
+      sum.x *= cf; sum.y *= cf; sum.z *= cf; sum.w *= cf;
+#else
+      sum.x /= cf; sum.y /= cf; sum.z /= cf; sum.w /= cf;
+#endif
+      if (vec_out && xx + 3 < W) {
+        *reinterpret_cast<float4*>(o4) = sum;
+      } else {
+        if (xx < W) o4[0] = sum.x;
+        if (xx + 1 < W) o4[1] = sum.y;
+        if (xx + 2 < W) o4[2] = sum.z;
+        if (xx + 3 < W) o4[3] = sum.w;
+      }
+    }
+  }
+}
+
+// One (tile, channel group) of gx1 (G2 == false: from g and x2) or gx2
+// (G2 == true: from g and x1; mirrored indices).
+template <int D, int PX, int SEGX, int NW, int CC, int V, bool G2, bool AM>
+__device__ __forceinline__ void corr_bwd_tile(float* sm, const float* __restrict__ xs,
+                                              const float* __restrict__ g,
+                                              float* __restrict__ gx, int tile, int group, int b,
+                                              int C, int H, int W, int tiles_x, int cg,
+                                              const BwdEpi& ep) {
+  using F = BwdCfg<D, PX, SEGX, NW, CC, V>;
+  constexpr int K = F::K, TW = F::TW, TH = F::TH, NT = F::NT;
+  constexpr int DYW = F::DYW, XIMG = F::XIMG;
+  (void)K;
+  float* red = sm + 2 * XIMG;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int cbeg = group * cg;
+  const int cend = min(C, cbeg + cg);
+  const int ty = tile / tiles_x;
+  const int tx = tile - ty * tiles_x;
+  const int y0 = ty * TH, x0 = tx * TW;
+  const int r = F::L::row(lane), q = F::L::seg(lane);
+  const int y = y0 + r;
+  const int xb = x0 + q * PX;
+
+  const int HW = H * W;
+  const float* xsb = xs + (size_t)b * C * HW;
+  // g of sample b at b * ep.g_bstride: a channel slice of the concat gradient,
+  // or the dense [B,K*K,H,W] tensor
+  float gv[DYW][2 * D + 1][PX];
+  bwd_load_g<D, PX, SEGX, NW, CC, V, G2, AM>(gv, g + (size_t)b * ep.g_bstride, ep, b, wave, y, xb, H, W);
   USF_TRACE_VMWAIT();
   USF_TRACE_AT(1);
+#ifdef USF_BWD_PROBE
+  // timing probes only (tools/ab_build.py): 1 = no g loads (runtime constants),
+  // 2 = g loads and the output store only (no channel stages)
+  if constexpr (USF_BWD_PROBE == 1) {
+#pragma unroll
+    for (int t = 0; t < DYW; ++t)
+#pragma unroll
+      for (int dx = 0; dx < 2 * D + 1; ++dx)
+#pragma unroll
+        for (int i = 0; i < PX; ++i) gv[t][dx][i] = ep.slope * (float)(t + dx + i);
+  }
+  if constexpr (USF_BWD_PROBE == 2) {
+    float sacc = 0.f;
+#pragma unroll
+    for (int t = 0; t < DYW; ++t)
+#pragma unroll
+      for (int dx = 0; dx < 2 * D + 1; ++dx)
+#pragma unroll
+        for (int i = 0; i < PX; ++i) sacc += gv[t][dx][i];
+    if (y < H && xb < W) gx[(size_t)b * C * HW + (size_t)(cbeg + wave) * HW + y * W + xb] = sacc;
+    return;
+  }
+#endif
 
   typename F::X sx;
   sx.init(wave, lane, y0 - D, x0 - D, H, W);
   const rsrc_t rx = plane_rsrc(xsb, true, C * HW * 4);
   auto dma_stage = [&](int c0, float* img) { sx.load(rx, img, wave, c0, cend, HW); };
 
-  const float cf = (float)C;
+  const float cf = USF_BWD_RCP ? 1.f / (float)C : (float)C;  // bwd_combine's scale
   float* gxb = gx + (size_t)b * C * HW;
-  const bool vec_out = (W & 3) == 0;
   dma_stage(cbeg, sm);
   dma_wait_all();
   __syncthreads();
@@ -792,65 +929,15 @@ __device__ __forceinline__ void corr_bwd_tile(float* sm, const float* __restrict
     const float* cur = sm + (st & 1) * XIMG;
     if (c0 + CC < cend) dma_stage(c0 + CC, sm + ((st + 1) & 1) * XIMG);
     USF_TRACE_AT(3 + 4 * st);
-    // partials stored lane-linear (lane*PX): conflict-free ds_write_b128
-    float* rp = red + wave * (CC * TH * TW) + lane * PX;
-#pragma unroll 2
-    for (int c = 0; c < CC; ++c) {
-      float acc[PX];
-#pragma unroll
-      for (int i = 0; i < PX; ++i) acc[i] = 0.f;
-#pragma unroll
-      for (int t = 0; t < DYW; ++t) {
-        const int dy = wave * DYW + t;
-        if (dy < K) {
-          const int rs = G2 ? (2 * D - dy) : dy;
-          float w[WIN];
-          lds_read<B64>(cur + c * P + (r + rs) * S + q * PX, w);
-#pragma unroll
-          for (int dx = 0; dx < K; ++dx) {
-            const int cs = G2 ? (2 * D - dx) : dx;
-#pragma unroll
-            for (int i = 0; i < PX; ++i) acc[i] = fmaf(gv[t][dx][i], w[i + cs], acc[i]);
-          }
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < PX / 4; ++i)
-        reinterpret_cast<float4*>(rp + c * (TH * TW))[i] =
-            make_float4(acc[4 * i], acc[4 * i + 1], acc[4 * i + 2], acc[4 * i + 3]);
-    }
+    bwd_stage<D, PX, SEGX, NW, CC, V, G2>(gv, cur, red + wave * (CC * TH * TW) + lane * PX, wave, r, q, ep);
     USF_TRACE_AT(4 + 4 * st);
     dma_wait_all();
     __syncthreads();  // partials complete; next stage's image landed
     USF_TRACE_AT(5 + 4 * st);
-    // combine the NW wave partials in a fixed order, 4 pixels per thread
-    // (a lane's PX pixels are contiguous in its partial slot)
-    for (int o = tid; o < CC * TH * TW / 4; o += NT) {
-      const int c = o / (TH * TW / 4);
-      const int pix = (o - c * (TH * TW / 4)) * 4;
-      const int py = pix / TW, pxo = pix % TW;
-      // lane that owns pixel (py, pxo) under the layout's lane mapping
-      const int ol = F::L::COLMAJOR ? (pxo / PX) * TH + py : py * SEGX + pxo / PX;
-      const int ridx = c * (TH * TW) + ol * PX + pxo % PX;
-      float4 sum = *reinterpret_cast<const float4*>(red + ridx);
-#pragma unroll
-      for (int w2 = 1; w2 < NW; ++w2) {
-        const float4 v = *reinterpret_cast<const float4*>(red + w2 * (CC * TH * TW) + ridx);
-        sum.x += v.x; sum.y += v.y; sum.z += v.z; sum.w += v.w;
-      }
-      const int yy = y0 + py, xx = x0 + pxo;
-      if (c0 + c < cend && yy < H) {
-        float* o4 = gxb + (size_t)(c0 + c) * HW + yy * W + xx;
-        if (vec_out && xx + 3 < W) {
-          *reinterpret_cast<float4*>(o4) = make_float4(sum.x / cf, sum.y / cf, sum.z / cf, sum.w / cf);
-        } else {
-          if (xx < W) o4[0] = sum.x / cf;
-          if (xx + 1 < W) o4[1] = sum.y / cf;
-          if (xx + 2 < W) o4[2] = sum.z / cf;
-          if (xx + 3 < W) o4[3] = sum.w / cf;
-        }
-      }
-    }
+#if defined(USF_BWD_PROBE) && USF_BWD_PROBE == 3
+    continue;  // probe: no combine, no second barrier (timing only)
+#endif
+    bwd_combine<D, PX, SEGX, NW, CC, V>(red, gxb, tid, NT, c0, cend, y0, x0, H, W, cf);
     __syncthreads();  // partial slices free for the next stage
     USF_TRACE_AT(6 + 4 * st);
   }
@@ -864,9 +951,6 @@ __device__ __forceinline__ void corr_bwd_tile(float* sm, const float* __restrict
 // 40 KB LDS, i.e. 3 waves/SIMD = 4 resident workgroups of 3 waves per CU.
 // amdgpu_waves_per_eu(3) pins the VGPR target: without it, allocation for the
 // two inlined direction bodies flips between 163 and 231 on unrelated edits.
-#ifndef USF_BWD_WAVES_PER_EU
-#define USF_BWD_WAVES_PER_EU 3
-#endif
 template <int D, int PX, int SEGX, int NW, int CC, int V, int MODE, bool AM>
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(USF_BWD_WAVES_PER_EU))) void corr_bwd_kernel(const float* __restrict__ x1,
                                                            const float* __restrict__ x2,
@@ -885,9 +969,6 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(USF_BWD
   // to the XCDs in contiguous chunks (L4 84 vs 59 us, L3 51 vs 43 us), although
   // they cut the FETCH traffic (2.6x -> 1.4x of algorithmic). Short chunks
   // (below) keep both.
-#ifndef USF_BWD_CHUNK
-#define USF_BWD_CHUNK 14
-#endif
   int w = linear_block();
   if (USF_BWD_CHUNK > 0 && gridDim.x >= 16) {
     // Q consecutive work items per XCD, chunks dealt round-robin over the 8
@@ -933,7 +1014,10 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(USF_BWD
 // Workgroups a backward launch aims for (both directions together): enough to
 // fill the 256 CUs at 3-4 resident workgroups each, and no more -- every
 // extra channel group re-reads its tile's slice of g (81 planes).
-constexpr int kBwdTargetWorkgroups = 768;
+#ifndef USF_BWD_TARGET_WG
+#define USF_BWD_TARGET_WG 768
+#endif
+constexpr int kBwdTargetWorkgroups = USF_BWD_TARGET_WG;
 
 template <int D, int PX, int SEGX, int NW, int CC, int V, int MODE>
 hipError_t launch_bwd_mode(const float* x1, const float* x2, const float* g, float* gx1,
