@@ -18,7 +18,8 @@
  *   usf_warp_fwd_f32  <- grid_sample(bilinear, align_corners=True) inside
  *                        flow_warp (utils/warp_utils.py:97-106, incl.
  *                        mesh_grid :7-13 and norm_grid :16-23)
- *   usf_warp_bwd_f32  <- grid_sampler_2d_backward reached from flow_warp's
+ *   usf_warp_bwd_f32 / usf_warp_bwd_ex_f32
+ *                     <- grid_sampler_2d_backward reached from flow_warp's
  *                        autograd graph (warp_utils.py:103-105)
  *   usf_splat_map_f32 <- get_corresponding_map (warp_utils.py:26-94,
  *                        scatter_add_ of bilinear weights)
@@ -64,7 +65,7 @@
 extern "C" {
 #endif
 
-#define USF_ABI_VERSION 4
+#define USF_ABI_VERSION 5
 #define USF_EINVAL (-1)
 
 /* padding modes for the warp (flow_warp `pad` argument) */
@@ -158,6 +159,24 @@ int usf_warp_fwd_f32(const float* x, const float* flow, long long flow_bstride,
 int usf_warp_bwd_f32(const float* x, const float* flow, long long flow_bstride,
                      const float* gout, float* gx, float* gflow,
                      int B, int C, int H, int W, int pad_mode, void* stream);
+
+/* usf_warp_bwd_f32 with a caller workspace of usf_warp_bwd_workspace(B,H,W)
+ * bytes (device memory, no alignment beyond 256 B needed; contents need not
+ * be initialised and are scratch after return). With it, gx is computed by
+ * a binned gather: every source pixel is filed under the cell of its
+ * north-west corner, then each target cell sums weight * gout over the
+ * pixels filed under it and its three up-left neighbours in a fixed order,
+ * and is written once -- no fp32 atomics and no zero fill, deterministic
+ * except for pixels beyond 4 per cell (strongly compressive flow), which are
+ * added with atomics afterwards. A smaller (or NULL) workspace falls back to
+ * the scatter of usf_warp_bwd_f32. */
+int usf_warp_bwd_ex_f32(const float* x, const float* flow, long long flow_bstride,
+                        const float* gout, float* gx, float* gflow, void* workspace,
+                        long long workspace_bytes, int B, int C, int H, int W, int pad_mode,
+                        void* stream);
+
+/* Workspace bytes usf_warp_bwd_ex_f32 uses for the binned gather. */
+long long usf_warp_bwd_workspace(int B, int H, int W);
 
 /* Forward bilinear splat of unit mass (get_corresponding_map,
  * utils/warp_utils.py:26-94): every source pixel p lands at

@@ -33,7 +33,8 @@ def test_header_declares_the_abi():
         ["usf_abi_version", "usf_last_error_string", "usf_corr_fwd_f32", "usf_corr_bwd_f32",
          "usf_corr_fwd_ex_f32", "usf_corr_fwd_workspace", "usf_corr_bwd_ex_f32", "usf_corr_act_mask_words",
          "usf_corr_bwd_ex_scratch",
-         "usf_warp_fwd_f32", "usf_warp_bwd_f32", "usf_splat_map_f32", "usf_occ_backward_f32",
+         "usf_warp_fwd_f32", "usf_warp_bwd_f32", "usf_warp_bwd_ex_f32", "usf_warp_bwd_workspace",
+         "usf_splat_map_f32", "usf_occ_backward_f32",
          "usf_occ_bidirection_f32",
          "usf_photo_loss_partials", "usf_photo_loss_fwd_f32", "usf_photo_loss_pair_fwd_f32",
          "usf_photo_loss_bwd_f32",
@@ -58,7 +59,7 @@ def test_library_exports_every_declared_symbol(lib):
 def test_abi_version(lib):
     from unsamflow_amd import _lib
 
-    assert lib.usf_abi_version() == _lib.ABI_VERSION == 4
+    assert lib.usf_abi_version() == _lib.ABI_VERSION == 5
 
 
 def test_no_torch_types_in_abi():
@@ -81,6 +82,8 @@ def test_no_torch_types_in_abi():
         (lambda L: L.usf_warp_fwd_f32(1, 1, 3, 1, 2, 3, 4, 4, 1, None), "batch stride"),
         (lambda L: L.usf_warp_bwd_f32(1, None, 32, 1, 1, 1, 1, 3, 4, 4, 1, None), "null input"),
         (lambda L: L.usf_warp_bwd_f32(1, 1, 32, 1, 1, 1, 1, 3, -4, 4, 1, None), "non-positive"),
+        (lambda L: L.usf_warp_bwd_ex_f32(1, 1, 32, 1, 1, 1, 1, -5, 1, 3, 4, 4, 1, None), "negative workspace"),
+        (lambda L: L.usf_warp_bwd_ex_f32(1, 1, 32, 1, 1, 1, 1, 64, 1, 3, 4, 4, 5, None), "pad_mode 5"),
         (lambda L: L.usf_corr_fwd_f32(1, 1, 1, 1, 70000, 200, 200, 4, None), "too large"),
         (lambda L: L.usf_corr_fwd_ex_f32(1, 1, 1, 10, 1, 0.1, None, None, 0, 2, 4, 4, 4, 4, None), "out batch stride"),
         (lambda L: L.usf_corr_fwd_ex_f32(1, 1, 1, 81 * 16, 7, 0.1, None, None, 0, 2, 4, 4, 4, 4, None), "unknown act"),
@@ -131,7 +134,7 @@ def test_variant_override_bounds(lib):
     assert n_fwd > 1 and n_bwd > 1
     assert lib.usf_set_variant(0, n_fwd) == -1 and b"bad op" in lib.usf_last_error_string()
     assert lib.usf_set_variant(3, 0) == -1
-    assert lib.usf_set_variant(2, 1) == 6 and lib.usf_set_variant(2, -1) == 6
+    assert lib.usf_set_variant(2, 1) == 7 and lib.usf_set_variant(2, -1) == 7
     assert lib.usf_set_variant(1, n_bwd - 1) == n_bwd
     assert lib.usf_set_variant(1, -1) == n_bwd
 
@@ -146,3 +149,13 @@ def test_ctypes_signatures_match_header():
         params = [p for p in m.group(1).split(",") if p.strip() and p.strip() != "void"]
         assert len(params) == len(argtypes), name
     assert ctypes.sizeof(ctypes.c_longlong) == 8
+
+
+def test_warp_bwd_workspace_size(lib):
+    """Workspace of the binned gather: counts, 4 slots (+ weights) per cell of the
+    (H+1) x (W+1) grid, overflow list; 0 for a non-positive shape."""
+    B, H, W = 16, 64, 208
+    n = lib.usf_warp_bwd_workspace(B, H, W)
+    cells = B * (H + 1) * (W + 1)
+    assert 4 * cells * (1 + 4 + 16) + 4 * B * H * W <= n <= 4 * cells * (1 + 4 + 16) + 4 * B * H * W + 5 * 256
+    assert lib.usf_warp_bwd_workspace(0, H, W) == 0

@@ -338,7 +338,7 @@ def test_corr_every_tile_variant_vs_oracle(hip_device, shape):
         lib.usf_set_variant(1, -1)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6])
 def test_warp_grad_x_scatter_variants(hip_device, variant):
     """Every grad_x variant (reduce-by-key atomics with any channel split,
     LDS-aggregated tiles, the gather with its outlier scatter) matches the
@@ -462,3 +462,48 @@ def test_warp_backward_default_large_levels(hip_device, shape, scale):
         rx, rf = warp_backward_np(x, flow, g, pad)
         np.testing.assert_allclose(_np(gx), rx, atol=1e-4, rtol=1e-5)
         np.testing.assert_allclose(_np(gf), rf, atol=1e-4, rtol=1e-5)
+
+
+@pytest.mark.parametrize("pad", ["border", "zeros"])
+def test_warp_binned_gather_deterministic_and_overflow(hip_device, pad):
+    """The default grad_x (binned gather, usf_warp_bwd_ex_f32): bit-identical
+    across runs for a smooth flow (no cell holds more than 4 source pixels), and
+    oracle-exact where most pixels overflow their cell (a flow contracting
+    every pixel towards the image centre, so whole regions share a cell and the
+    atomic overflow pass carries them)."""
+    from unsamflow_amd import ops
+
+    B, C, H, W = 2, 8, 40, 64
+    x = hashrng.uniform((B, C, H, W), 700)
+    g = hashrng.normal((B, C, H, W), 701)
+    yy, xx = np.meshgrid(np.arange(H, dtype=np.float32), np.arange(W, dtype=np.float32), indexing="ij")
+    smooth = np.stack([1.7 * np.sin(xx / 9.0) + 0.3, 1.2 * np.cos(yy / 7.0) - 0.4])[None].repeat(B, 0)
+    contract = np.stack([0.9 * ((W - 1) / 2.0 - xx), 0.9 * ((H - 1) / 2.0 - yy)])[None].repeat(B, 0)
+    for flow, deterministic in ((smooth.astype(np.float32), True), (contract.astype(np.float32), False)):
+        tx, tf, tg = _dev(x, hip_device), _dev(flow, hip_device), _dev(g, hip_device)
+        gx, gf = ops.warp_backward(tx, tf, tg, pad)
+        rx, rf = warp_backward_np(x, flow, g, pad)
+        np.testing.assert_allclose(_np(gx), rx, atol=1e-4, rtol=1e-5)
+        np.testing.assert_allclose(_np(gf), rf, atol=1e-4, rtol=1e-5)
+        if deterministic:
+            gx2, _ = ops.warp_backward(tx, tf, tg, pad)
+            assert torch.equal(gx, gx2)
+
+
+def test_warp_bwd_plain_entry_is_the_scatter(hip_device):
+    """usf_warp_bwd_f32 (no workspace) keeps the atomic scatter and matches the oracle."""
+    from unsamflow_amd import _lib
+
+    lib = _lib.load()
+    shape = (2, 16, 24, 40)
+    x = hashrng.uniform(shape, 710)
+    flow = hashrng.symmetric((2, 2, 24, 40), 711, 3.0)
+    g = hashrng.normal(shape, 712)
+    tx, tf, tg = _dev(x, hip_device), _dev(flow, hip_device), _dev(g, hip_device)
+    gx, gf = torch.empty_like(tx), torch.empty(2, 2, 24, 40, device=hip_device)
+    rc = lib.usf_warp_bwd_f32(tx.data_ptr(), tf.data_ptr(), 2 * 24 * 40, tg.data_ptr(), gx.data_ptr(),
+                              gf.data_ptr(), *shape, _lib.PAD_BORDER, _lib.stream_handle(hip_device))
+    _lib.check(rc, "usf_warp_bwd_f32")
+    rx, rf = warp_backward_np(x, flow, g, "border")
+    np.testing.assert_allclose(_np(gx), rx, atol=1e-4, rtol=1e-5)
+    np.testing.assert_allclose(_np(gf), rf, atol=1e-4, rtol=1e-5)

@@ -244,28 +244,51 @@ int usf_warp_fwd_f32(const float* x, const float* flow, long long flow_bstride, 
                 (hipStream_t)stream);
 }
 
-int usf_warp_bwd_f32(const float* x, const float* flow, long long flow_bstride,
-                     const float* gout, float* gx, float* gflow, int B, int C, int H, int W,
-                     int pad_mode, void* stream) {
+static int warp_bwd_common(const char* fn, const float* x, const float* flow, long long flow_bstride,
+                           const float* gout, float* gx, float* gflow, void* ws, long long ws_bytes, int B,
+                           int C, int H, int W, int pad_mode, void* stream) {
   clear_error();
-  if (!check_dims("usf_warp_bwd_f32", B, C, H, W)) return USF_EINVAL;
+  if (!check_dims(fn, B, C, H, W)) return USF_EINVAL;
   if (pad_mode != USF_PAD_ZEROS && pad_mode != USF_PAD_BORDER) {
-    set_error("usf_warp_bwd_f32: unknown pad_mode %d", pad_mode);
+    set_error("%s: unknown pad_mode %d", fn, pad_mode);
     return USF_EINVAL;
   }
   if (!flow || !gout || (gflow && !x)) {
-    set_error("usf_warp_bwd_f32: null input pointer");
+    set_error("%s: null input pointer", fn);
     return USF_EINVAL;
   }
   if (flow_bstride < 2LL * H * W && B > 1) {
-    set_error("usf_warp_bwd_f32: flow batch stride %lld < 2*H*W", flow_bstride);
+    set_error("%s: flow batch stride %lld < 2*H*W", fn, flow_bstride);
     return USF_EINVAL;
   }
-  if (const int pe = pre_check("usf_warp_bwd_f32", (hipStream_t)stream)) return pe;
-  return finish("usf_warp_bwd_f32",
+  if (ws_bytes < 0) {
+    set_error("%s: negative workspace size", fn);
+    return USF_EINVAL;
+  }
+  if (const int pe = pre_check(fn, (hipStream_t)stream)) return pe;
+  return finish(fn,
                 warp_bwd_launch(x, flow, flow_bstride, gout, gx, gflow, B, C, H, W, pad_mode,
-                                (hipStream_t)stream),
+                                (hipStream_t)stream, ws, ws_bytes),
                 (hipStream_t)stream);
+}
+
+int usf_warp_bwd_f32(const float* x, const float* flow, long long flow_bstride,
+                     const float* gout, float* gx, float* gflow, int B, int C, int H, int W,
+                     int pad_mode, void* stream) {
+  return warp_bwd_common("usf_warp_bwd_f32", x, flow, flow_bstride, gout, gx, gflow, nullptr, 0, B, C, H, W,
+                         pad_mode, stream);
+}
+
+int usf_warp_bwd_ex_f32(const float* x, const float* flow, long long flow_bstride, const float* gout,
+                        float* gx, float* gflow, void* workspace, long long workspace_bytes, int B, int C,
+                        int H, int W, int pad_mode, void* stream) {
+  return warp_bwd_common("usf_warp_bwd_ex_f32", x, flow, flow_bstride, gout, gx, gflow, workspace,
+                         workspace ? workspace_bytes : 0, B, C, H, W, pad_mode, stream);
+}
+
+long long usf_warp_bwd_workspace(int B, int H, int W) {
+  if (B <= 0 || H <= 0 || W <= 0) return 0;
+  return warp_bwd_workspace(B, H, W);
 }
 
 static bool check_splat(const char* fn, const float* flow, long long fbs, const float* out, int B,

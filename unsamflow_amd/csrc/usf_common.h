@@ -94,7 +94,10 @@ hipError_t warp_fwd_launch(const float* x, const float* flow, long long flow_bst
                            hipStream_t s);
 hipError_t warp_bwd_launch(const float* x, const float* flow, long long flow_bstride,
                            const float* gout, float* gx, float* gflow, int B, int C, int H,
-                           int W, int pad_mode, hipStream_t s);
+                           int W, int pad_mode, hipStream_t s, void* workspace = nullptr,
+                           long long workspace_bytes = 0);
+// bytes of workspace for the binned-gather grad_x (usf_warp_bwd_ex_f32)
+long long warp_bwd_workspace(int B, int H, int W);
 
 hipError_t splat_launch(const float* flow, long long flow_bstride, float* map, int B, int H, int W,
                         bool absolute, hipStream_t s);

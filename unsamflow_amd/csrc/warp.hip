@@ -266,14 +266,34 @@ __device__ __forceinline__ bool gather_inlier(float u, float v) {
   return fabsf(u) < (float)kGatherR && fabsf(v) < (float)kGatherR;  // false for NaN
 }
 
-template <bool BORDER, bool WANT_GX, bool WANT_GF, int CS, bool OUTL = false>
+// grad_x by a binned gather (the default with a caller workspace,
+// usf_warp_bwd_ex_f32). Each source pixel p is filed, by the first pass, under
+// its north-west corner cell nw(p) (a cell grid extended by one row and column
+// above / left of the image, so corners at -1 are addressable): up to kBinSlots
+// pixels per cell, the rest on an overflow list. The gather pass then gives
+// every target cell q exactly the pixels filed under q, q - (0,1), q - (1,0)
+// and q - (1,1) -- those whose NW, NE, SW or SE corner is q -- in a fixed order
+// (corner, then pixel index), and writes gx[c][q] once: no float atomics, no
+// zero fill, deterministic. Overflow pixels (more than kBinSlots sharing one
+// cell: strongly compressive flow, or border clamping) are listed and added
+// afterwards with float atomics.
+constexpr int kBinSlots = 4;
+struct BinArgs {
+  int* cnt = nullptr;      // [B][(H+1)(W+1)] pixels filed per cell
+  int* bins = nullptr;     // [B][(H+1)(W+1)][kBinSlots] source pixel (py << 16 | px)
+  float4* wbin = nullptr;  // [B][(H+1)(W+1)][kBinSlots] its corner weights (nw, ne, sw, se), 0 off-image
+  int* ovf = nullptr;      // [B * HW] overflow list: b * HW + p
+  int* novf = nullptr;     // overflow list length
+};
+
+template <bool BORDER, bool WANT_GX, bool WANT_GF, int CS, int OUTL = 0, bool BIN = false>
 __global__ __launch_bounds__(256) void warp_bwd_kernel(const float* __restrict__ x,
                                                        const float* __restrict__ flow,
                                                        long long fbs,
                                                        const float* __restrict__ gout,
                                                        float* __restrict__ gx,
                                                        float* __restrict__ gflow, int B, int C,
-                                                       int H, int W) {
+                                                       int H, int W, BinArgs ba = {}) {
   constexpr int PXB = 256 / CS;
   __shared__ float red[2][256];
   const int HW = H * W;
@@ -290,11 +310,25 @@ __global__ __launch_bounds__(256) void warp_bwd_kernel(const float* __restrict__
     const int y = p / W, xx = p - y * W;
     const float* fb = flow + b * fbs;
     const float u = fb[p], v = fb[HW + p];
-    if (OUTL) valid = !gather_inlier(u, v);  // the gather kernel has the inliers
+    if (OUTL == 1) valid = !gather_inlier(u, v);  // the gather kernel has the inliers
     tp = make_tap(u, v, xx, y, H, W, BORDER);
   }
   if (!valid) tp.m_nw = tp.m_ne = tp.m_sw = tp.m_se = false;
   if (OUTL && !__syncthreads_or(valid)) return;  // no outlier in this workgroup (uniform)
+  if (BIN && slice == 0 && valid) {
+    // file p under its north-west corner cell (see BinArgs); weights as the scatter forms them
+    if (tp.m_nw || tp.m_ne || tp.m_sw || tp.m_se) {  // then xw in [-1, W), yn in [-1, H)
+      const size_t cell = (size_t)b * (H + 1) * (W + 1) + (size_t)(tp.yn + 1) * (W + 1) + (tp.xw + 1);
+      const int slot = atomicAdd(ba.cnt + cell, 1);
+      if (slot < kBinSlots) {
+        ba.bins[cell * kBinSlots + slot] = (p / W) << 16 | (p % W);  // (py, px): sorts as p
+        ba.wbin[cell * kBinSlots + slot] = make_float4(tp.m_nw ? tp.s * tp.e : 0.f, tp.m_ne ? tp.s * tp.w : 0.f,
+                                                       tp.m_sw ? tp.n * tp.e : 0.f, tp.m_se ? tp.n * tp.w : 0.f);
+      } else {
+        ba.ovf[atomicAdd(ba.novf, 1)] = b * HW + p;  // scattered by the overflow pass
+      }
+    }
+  }
   // grad_x: reduce-by-key over the wave per corner row (see scatter_row)
   RowRuns rn{}, rs{};
   if (WANT_GX) {
@@ -353,6 +387,202 @@ __global__ __launch_bounds__(256) void warp_bwd_kernel(const float* __restrict__
     float* gf = gflow + (size_t)b * 2 * HW + p;
     gf[0] = (ggx / (float)(W - 1)) * 2.0f;
     gf[HW] = (ggy / (float)(H - 1)) * 2.0f;
+  }
+}
+
+// The gather pass of the binned grad_x: thread = target cell q, channels
+// [c0, c0 + cper) of sample b. For corner k (0 NW, 1 NE, 2 SW, 3 SE) the
+// pixels filed under q - (k / 2, k % 2) are sorted by index (at most
+// kBinSlots), and each channel sums weight * gout over them in that order.
+// Slot loops run to the wave's largest count (uniform), so every register
+// index is static.
+constexpr int kGatherCH = 8;  // channels per pass of the binned gather
+__device__ __forceinline__ void cswap(int& a, int& b) {
+  const int lo = min(a, b), hi = max(a, b);
+  a = lo;
+  b = hi;
+}
+// Target tile of the gather pass: 32 x 8 cells (thread t: column t % 32, row
+// t / 32); the box of all its source pixels (one per entry) is staged in LDS
+// per pass of kGatherCH channels when it holds at most kBoxCap pixels
+// (smooth flows: the tile shifted by the local flow, plus its spread), else
+// the sources are read from global memory directly.
+constexpr int kBinTW = 32, kBinTH = 8;
+constexpr int kBoxW = 64, kBoxH = 16;  // staged box: rows of kBoxW floats (lane = column)
+constexpr int kBoxCap = kBoxW * kBoxH;
+__global__ __launch_bounds__(256) void warp_gx_bins_kernel(const float* __restrict__ gout, BinArgs ba,
+                                                           float* __restrict__ gx, int C, int H, int W,
+                                                           int tiles_x, int cper) {
+  static_assert(kBinSlots == 4, "sorting network for 4 slots");
+  __shared__ float box[kGatherCH * kBoxCap];
+  __shared__ int bb[4];  // source box: y min, y max, x min, x max
+  const int HW = H * W, W1 = W + 1, E = (H + 1) * W1;
+  const int t = threadIdx.x;
+  const int ty0 = (blockIdx.x / tiles_x) * kBinTH, tx0 = (blockIdx.x % tiles_x) * kBinTW;
+  const int qy = ty0 + t / kBinTW, qx = tx0 + t % kBinTW;
+  const int b = blockIdx.y;
+  const int c0 = blockIdx.z * cper, c1 = min(C, c0 + cper);
+  const bool valid = qy < H && qx < W;
+  const int qq = valid ? qy * W + qx : 0;
+  if (t == 0) {
+    bb[0] = INT_MAX; bb[1] = INT_MIN; bb[2] = INT_MAX; bb[3] = INT_MIN;
+  }
+  // entries: packed (py << 16 | px) of the sources filed under the four cells
+  int pk[4][kBinSlots];
+  float wk[4][kBinSlots];
+  int nmax[4];
+  int ylo = INT_MAX, yhi = INT_MIN, xlo = INT_MAX, xhi = INT_MIN;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const size_t cell = (size_t)b * E + (size_t)(qy - (k >> 1) + 1) * W1 + (qx - (k & 1) + 1);
+    // count, slots and the slots' weights load together (slots 0 and 1
+    // unconditionally: most cells hold at most two pixels)
+    const size_t ce = valid ? cell : 0;
+    const int n = valid ? min(ba.cnt[ce], kBinSlots) : 0;
+    const int4 e4 = *reinterpret_cast<const int4*>(ba.bins + ce * kBinSlots);
+    const float4* wb = ba.wbin + ce * kBinSlots;
+    float wv[kBinSlots];
+#pragma unroll
+    for (int j = 0; j < kBinSlots; ++j) {
+      const float4 w4 = (j < 2 || j < n) ? wb[j] : make_float4(0.f, 0.f, 0.f, 0.f);
+      wv[j] = j < n ? (k == 0 ? w4.x : k == 1 ? w4.y : k == 2 ? w4.z : w4.w) : 0.f;
+    }
+    pk[k][0] = n > 0 ? e4.x : INT_MAX;
+    pk[k][1] = n > 1 ? e4.y : INT_MAX;
+    pk[k][2] = n > 2 ? e4.z : INT_MAX;
+    pk[k][3] = n > 3 ? e4.w : INT_MAX;
+    // sort the (pixel, weight) pairs by pixel: the summation order is fixed
+    auto cs2 = [&](int i, int j) {
+      const bool sw = pk[k][j] < pk[k][i];
+      const int pi = pk[k][i], pj = pk[k][j];
+      const float wi = wv[i], wj = wv[j];
+      pk[k][i] = sw ? pj : pi; pk[k][j] = sw ? pi : pj;
+      wv[i] = sw ? wj : wi; wv[j] = sw ? wi : wj;
+    };
+    cs2(0, 1); cs2(2, 3); cs2(0, 2); cs2(1, 3); cs2(1, 2);
+#pragma unroll
+    for (int j = 0; j < kBinSlots; ++j) {
+      const bool has = j < n;
+      const int py = has ? pk[k][j] >> 16 : qy, px = has ? pk[k][j] & 0xFFFF : qx;
+      wk[k][j] = wv[j];
+      pk[k][j] = (py << 16) | px;
+      if (has) {
+        ylo = min(ylo, py); yhi = max(yhi, py); xlo = min(xlo, px); xhi = max(xhi, px);
+      }
+    }
+    int m = n;  // the wave's largest count for this corner
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = max(m, __shfl_xor(m, o));
+    nmax[k] = m;
+  }
+  // the workgroup's source box: wave reduction, then one LDS atomic per wave
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    ylo = min(ylo, __shfl_xor(ylo, o)); yhi = max(yhi, __shfl_xor(yhi, o));
+    xlo = min(xlo, __shfl_xor(xlo, o)); xhi = max(xhi, __shfl_xor(xhi, o));
+  }
+  __syncthreads();  // bb initialised
+  if ((t & 63) == 0 && ylo <= yhi) {
+    atomicMin(&bb[0], ylo); atomicMax(&bb[1], yhi); atomicMin(&bb[2], xlo); atomicMax(&bb[3], xhi);
+  }
+  __syncthreads();
+  const int by0 = bb[0], bx0 = bb[2];
+  const int bh = bb[1] - by0 + 1, bw = bb[3] - bx0 + 1;
+  const bool staged = bb[0] <= bb[1] && bh <= kBoxH && bw <= kBoxW;  // workgroup-uniform
+  const float* gb = gout + (size_t)b * C * HW;
+  float* gq = gx + (size_t)b * C * HW + qq;
+  // per entry: offset into the staged box, or the plane offset
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+#pragma unroll
+    for (int j = 0; j < kBinSlots; ++j) {
+      const int py = pk[k][j] >> 16, px = pk[k][j] & 0xFFFF;
+      pk[k][j] = staged ? (py - by0) * kBoxW + (px - bx0) : py * W + px;
+    }
+  // kGatherCH channels per pass with independent accumulators
+  for (int c = c0; c < c1; c += kGatherCH) {
+    float acc[kGatherCH];
+#pragma unroll
+    for (int u = 0; u < kGatherCH; ++u) acc[u] = 0.f;
+    if (staged) {
+      __syncthreads();  // the previous pass is done with the box
+      // box rows (channel u, row yy) dealt to the 4 waves, lanes along x
+      // (coalesced); every row load of a wave is issued before any store
+      constexpr int kRows = kGatherCH * kBoxH / 4;  // rows per wave, at most
+      constexpr int kHalf = kRows / 2;               // issued together (VGPR budget)
+      const int wv = t >> 6, ln = t & 63;
+      int u = 0, yy = wv;  // row wv + 4 i = u * bh + yy
+      for (int h = 0; h < 2 && u < kGatherCH; ++h) {
+        float v[kHalf];
+        int uu = u, y2 = yy;
+#pragma unroll
+        for (int i = 0; i < kHalf; ++i) {
+          while (y2 >= bh) { y2 -= bh; ++uu; }
+          const bool ok = uu < kGatherCH && c + uu < c1 && ln < bw;
+          v[i] = ok ? gb[(size_t)(c + uu) * HW + (by0 + y2) * W + bx0 + ln] : 0.f;
+          y2 += 4;
+        }
+#pragma unroll
+        for (int i = 0; i < kHalf; ++i) {
+          while (yy >= bh) { yy -= bh; ++u; }
+          if (u < kGatherCH) box[u * kBoxCap + yy * kBoxW + ln] = v[i];
+          yy += 4;
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int j = 0; j < kBinSlots; ++j)
+          if (j < nmax[k]) {
+#pragma unroll
+            for (int u = 0; u < kGatherCH; ++u) acc[u] = fmaf(wk[k][j], box[u * kBoxCap + pk[k][j]], acc[u]);
+          }
+    } else {
+      int co[kGatherCH];  // channel offsets, clamped into the group (extra lanes load, never store)
+#pragma unroll
+      for (int u = 0; u < kGatherCH; ++u) co[u] = min(c + u, c1 - 1) * HW;
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int j = 0; j < kBinSlots; ++j)
+          if (j < nmax[k]) {
+            const float* src = gb + pk[k][j];
+#pragma unroll
+            for (int u = 0; u < kGatherCH; ++u) acc[u] = fmaf(wk[k][j], src[co[u]], acc[u]);
+          }
+    }
+    if (valid) {
+#pragma unroll
+      for (int u = 0; u < kGatherCH; ++u)
+        if (c + u < c1) gq[(size_t)(c + u) * HW] = acc[u];
+    }
+  }
+}
+
+// Overflow pixels of the binned grad_x add their four corner contributions
+// with float atomics after the gather pass (thread = list entry x channel;
+// the loop bound is the device-side list length, so the kernel exits at once
+// when nothing overflowed).
+template <bool BORDER>
+__global__ __launch_bounds__(256) void warp_gx_ovf_kernel(const float* __restrict__ flow, long long fbs,
+                                                          const float* __restrict__ gout, BinArgs ba,
+                                                          float* __restrict__ gx, int C, int H, int W) {
+  const int HW = H * W;
+  const long long total = (long long)(*ba.novf) * C;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+    const int ent = ba.ovf[i / C];
+    const int c = (int)(i % C);
+    const int b = ent / HW, p = ent - b * HW;
+    const int y = p / W, xx = p - y * W;
+    const float* fb = flow + b * fbs;
+    const Tap tp = make_tap(fb[p], fb[HW + p], xx, y, H, W, BORDER);
+    const float go = gout[((size_t)b * C + c) * HW + p];
+    float* gc = gx + ((size_t)b * C + c) * HW;
+    if (tp.m_nw) atomicAdd(gc + tp.o_nw, go * (tp.s * tp.e));
+    if (tp.m_ne) atomicAdd(gc + tp.o_ne, go * (tp.s * tp.w));
+    if (tp.m_sw) atomicAdd(gc + tp.o_sw, go * (tp.n * tp.e));
+    if (tp.m_se) atomicAdd(gc + tp.o_se, go * (tp.n * tp.w));
   }
 }
 
@@ -715,16 +945,92 @@ void bwd_gather_cs(const float* x, const float* flow, long long fbs, const float
   const int cgroups = (C + cper - 1) / cper;
   hipLaunchKernelGGL((warp_gx_gather_kernel<BORDER>), dim3((unsigned)(tiles_x * tiles_y), (unsigned)(B * cgroups)),
                      block, 0, s, flow, fbs, gout, gx, C, H, W, tiles_x, cgroups, cper);
-  hipLaunchKernelGGL((warp_bwd_kernel<BORDER, true, false, CS, true>), grid, block, 0, s, x, flow, fbs, gout,
+  hipLaunchKernelGGL((warp_bwd_kernel<BORDER, true, false, CS, 1>), grid, block, 0, s, x, flow, fbs, gout,
                      gx, nullptr, B, C, H, W);
+}
+
+// Binned-gather workspace: overflow count and cell counts (zeroed per call),
+// cell slots with their weights, overflow list.
+struct BinLayout {
+  long long novf_off, cnt_off, bins_off, wbin_off, ovf_off, total;
+};
+inline BinLayout bin_layout(int B, int H, int W) {
+  auto al = [](long long v) { return (v + 255) & ~255LL; };
+  const long long E = (long long)B * (H + 1) * (W + 1), P = (long long)B * H * W;
+  BinLayout L;
+  L.novf_off = 0;
+  L.cnt_off = 256;
+  L.bins_off = al(L.cnt_off + 4 * E);
+  L.wbin_off = al(L.bins_off + 4 * E * kBinSlots);
+  L.ovf_off = al(L.wbin_off + 16 * E * kBinSlots);
+  L.total = al(L.ovf_off + 4 * P);
+  return L;
+}
+
+template <bool BORDER, int CS>
+void bin_pass_cs(const float* x, const float* flow, long long fbs, const float* gout, float* gflow, int B,
+                 int C, int H, int W, BinArgs ba, hipStream_t s) {
+  const dim3 grid((unsigned)((H * W + 256 / CS - 1) / (256 / CS)), (unsigned)B), block(256);
+  if (gflow)
+    hipLaunchKernelGGL((warp_bwd_kernel<BORDER, false, true, CS, false, true>), grid, block, 0, s, x, flow, fbs,
+                       gout, nullptr, gflow, B, C, H, W, ba);
+  else
+    hipLaunchKernelGGL((warp_bwd_kernel<BORDER, false, false, CS, false, true>), grid, block, 0, s, x, flow,
+                       fbs, gout, nullptr, nullptr, B, C, H, W, ba);
+}
+
+// grad_x by the binned gather (+ grad_flow in the filing pass); see BinArgs.
+template <bool BORDER>
+void bwd_bins(const float* x, const float* flow, long long fbs, const float* gout, float* gx, float* gflow, int B,
+              int C, int H, int W, void* ws, hipStream_t s) {
+  const BinLayout L = bin_layout(B, H, W);
+  char* w = static_cast<char*>(ws);
+  BinArgs ba;
+  ba.cnt = reinterpret_cast<int*>(w + L.cnt_off);
+  ba.bins = reinterpret_cast<int*>(w + L.bins_off);
+  ba.wbin = reinterpret_cast<float4*>(w + L.wbin_off);
+  ba.ovf = reinterpret_cast<int*>(w + L.ovf_off);
+  ba.novf = reinterpret_cast<int*>(w + L.novf_off);
+  (void)hipMemsetAsync(w, 0, (size_t)(L.cnt_off + 4LL * B * (H + 1) * (W + 1)), s);  // novf + counts
+  // filing pass, with grad_flow's channel slices chosen as for the scatter
+  const long runs64 = (long)B * ((H * W + 63) / 64);
+  const int cs = (runs64 >= 96 && C >= 4) ? 4 : pick_cs(B, C, H * W);
+  switch (cs) {
+    case 1: bin_pass_cs<BORDER, 1>(x, flow, fbs, gout, gflow, B, C, H, W, ba, s); break;
+    case 4: bin_pass_cs<BORDER, 4>(x, flow, fbs, gout, gflow, B, C, H, W, ba, s); break;
+    case 16: bin_pass_cs<BORDER, 16>(x, flow, fbs, gout, gflow, B, C, H, W, ba, s); break;
+    default: bin_pass_cs<BORDER, 64>(x, flow, fbs, gout, gflow, B, C, H, W, ba, s); break;
+  }
+  // gather pass: 32 x 8 target tiles, channel groups (multiples of kGatherCH)
+  // until ~2048 workgroups
+  const int tiles_x = (W + kBinTW - 1) / kBinTW, ntiles = tiles_x * ((H + kBinTH - 1) / kBinTH);
+  const long units = (long)ntiles * B;
+  const int chunks = (C + kGatherCH - 1) / kGatherCH;
+#ifndef USF_BIN_WGS
+#define USF_BIN_WGS 2048
+#endif
+  const int want = (int)std::min<long>(chunks, std::max<long>(1, (USF_BIN_WGS + units - 1) / units));
+  const int cper = ((chunks + want - 1) / want) * kGatherCH;
+  const int zg = (C + cper - 1) / cper;
+  hipLaunchKernelGGL(warp_gx_bins_kernel, dim3((unsigned)ntiles, (unsigned)B, (unsigned)zg), dim3(256), 0, s, gout,
+                     ba, gx, C, H, W, tiles_x, cper);
+  // overflow pixels (few or none for smooth flows): listed, scattered with atomics
+  hipLaunchKernelGGL((warp_gx_ovf_kernel<BORDER>), dim3(256), dim3(256), 0, s, flow, fbs, gout, ba, gx, C, H, W);
 }
 
 template <bool BORDER>
 void bwd_launch_pad(const float* x, const float* flow, long long fbs, const float* gout,
-                    float* gx, float* gflow, int B, int C, int H, int W, hipStream_t s) {
+                    float* gx, float* gflow, int B, int C, int H, int W, hipStream_t s,
+                    void* ws = nullptr, long long ws_bytes = 0) {
   // usf_set_variant(2, 2 / 3): lane-merged scatter with CS forced to 4 / 1
   // (whole-wave pixel runs) instead of the occupancy-driven choice
   const int v = variant_override(2);
+  // binned gather (default with a workspace; usf_set_variant(2, 6) requires one)
+  // (bin entries pack (py, px) into 16-bit halves)
+  if (gx && ws && ws_bytes >= bin_layout(B, H, W).total && (v < 0 || v == 6) && H < 32768 && W < 65536) {
+    bwd_bins<BORDER>(x, flow, fbs, gout, gx, gflow, B, C, H, W, ws, s);
+    return;
+  }
   // usf_set_variant(2, 4): deterministic gather for grad_x. Measured against the
   // lane-merged scatter at the decoder's batch-16 shapes (profiles/ab_r01/
   // warp_gather.json): faster for near-zero flows (L4 53 vs 81 us, L1 21 vs
@@ -932,14 +1238,16 @@ hipError_t warp_fwd_launch(const float* x, const float* flow, long long fbs, flo
 
 hipError_t warp_bwd_launch(const float* x, const float* flow, long long fbs, const float* gout,
                            float* gx, float* gflow, int B, int C, int H, int W, int pad_mode,
-                           hipStream_t s) {
+                           hipStream_t s, void* ws, long long ws_bytes) {
   if (!gx && !gflow) return hipSuccess;
   if (pad_mode == 1)
-    bwd_launch_pad<true>(x, flow, fbs, gout, gx, gflow, B, C, H, W, s);
+    bwd_launch_pad<true>(x, flow, fbs, gout, gx, gflow, B, C, H, W, s, ws, ws_bytes);
   else
-    bwd_launch_pad<false>(x, flow, fbs, gout, gx, gflow, B, C, H, W, s);
+    bwd_launch_pad<false>(x, flow, fbs, gout, gx, gflow, B, C, H, W, s, ws, ws_bytes);
   return hipGetLastError();
 }
+
+long long warp_bwd_workspace(int B, int H, int W) { return bin_layout(B, H, W).total; }
 
 hipError_t splat_launch(const float* flow, long long fbs, float* map, int B, int H, int W,
                         bool absolute, hipStream_t s) {

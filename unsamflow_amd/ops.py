@@ -192,15 +192,18 @@ def warp_backward(
     gx = torch.empty_like(xc) if need_x else None  # overwritten by the library
     gf = torch.empty((B, 2, H, W), device=x.device, dtype=torch.float32) if need_flow else None
     lib = _lib.load()
+    # grad_x by the binned gather: its workspace comes from torch's caching allocator
+    nws = int(lib.usf_warp_bwd_workspace(B, H, W)) if need_x else 0
+    ws = torch.empty(nws, device=x.device, dtype=torch.uint8) if nws > 0 else None
     with torch.cuda.device(x.device), _kt.timed(
         "warp_bwd", (B, C, H, W, pad, need_x, need_flow), x.device,
         _kt.warp_bytes(B, C, H, W, True, need_x, need_flow),
     ):
-        rc = lib.usf_warp_bwd_f32(
-            xc.data_ptr(), fv.data_ptr(), fbs, gc.data_ptr(), _ptr(gx), _ptr(gf),
+        rc = lib.usf_warp_bwd_ex_f32(
+            xc.data_ptr(), fv.data_ptr(), fbs, gc.data_ptr(), _ptr(gx), _ptr(gf), _ptr(ws), nws,
             B, C, H, W, PAD_MODES[pad], _lib.stream_handle(x.device),
         )
-    _lib.check(rc, "usf_warp_bwd_f32")
+    _lib.check(rc, "usf_warp_bwd_ex_f32")
     return gx, gf
 
 
