@@ -52,7 +52,7 @@ def test_corr_leaky_cat_matches_composition(hip_device, B, C, H, W, n_pairs):
 @pytest.mark.parametrize("B,C,H,W", [(2, 32, 64, 208), (2, 64, 32, 104), (8, 96, 16, 52), (1, 8, 5, 4), (3, 16, 7, 12),
                                      (16, 192, 4, 13), (16, 128, 8, 26), (2, 8, 3, 5), (1, 4, 9, 1)])
 def test_sign_mask_derivative_equals_dense_pass(hip_device, B, C, H, W):
-    """The forward's LeakyReLU sign mask (epilogue, or the mask kernel after the
+    """The forward's LeakyReLU sign mask (epilogue, or the atomic OR of the
     channel-split reduce at (8, 96, 16, 52) and the KITTI L0/L1 shapes; widths
     that are not a multiple of 4 included) equals (activated output > 0) bit
     for bit, and the backward that applies the derivative from it inside its

@@ -378,12 +378,20 @@ __global__ __launch_bounds__(64 * NDY) void corr_fwd_kernel(const float* __restr
     USF_TRACE_AT(5 + 4 * st);
   }
 
+  if (G > 1 && ep.act && ep.mask) {
+    // split forward: zero the sign mask here (every thread of the grid takes
+    // part); corr_fwd_reduce_kernel, launched after this kernel, ORs its bits in
+    const long long nw = (long long)(gridDim.z / G) * K * H * ((W + 3) >> 2);
+    const long long nt = (long long)gridDim.x * gridDim.y * gridDim.z * blockDim.x;
+    for (long long i = (long long)linear_block() * blockDim.x + threadIdx.x; i < nw; i += nt) ep.mask[i] = 0ull;
+  }
   if (!active) return;
   const int y = y0 + r;
   if (y >= H) return;
   const int xb = x0 + q * PX;
   if (G > 1) {  // raw channel-group partials [g][b][k][p]; corr_fwd_reduce_kernel finishes
     const int Bn = gridDim.z / G;
+
     float* pb = ep.part + ((size_t)(grp * Bn + b) * K * K + (size_t)dy * K) * HW + y * W + xb;
     const bool pvec = ((W & 3) == 0) && (xb + PX <= W);
 #pragma unroll
@@ -450,37 +458,21 @@ __global__ __launch_bounds__(64 * NDY) void corr_fwd_kernel(const float* __restr
   }
 }
 
-// The sign mask of FwdEpi::mask from the activated output itself, for the
-// channel-split forward (its reduce kernel applies the epilogue element-wise):
-// one thread per (b, dy, y, quad) reads the 9 dx planes' 4-pixel runs.
-template <int K>
-__global__ __launch_bounds__(256) void corr_act_mask_kernel(const float* __restrict__ out,
-                                                            long long obs,
-                                                            unsigned long long* __restrict__ mask,
-                                                            int B, int H, int W) {
-  const int W4 = (W + 3) >> 2;
-  const long long n = (long long)B * K * H * W4;
-  const long long t = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (t >= n) return;
-  const int qd = (int)(t % W4);
-  const long long row = t / W4;  // (b * K + dy) * H + y
-  const int y = (int)(row % H);
-  const int dy = (int)((row / H) % K);
-  const int b = (int)(row / ((long long)H * K));
-  const float* o = out + (size_t)b * obs + (size_t)dy * K * H * W + (size_t)y * W + 4 * qd;
-  unsigned long long bits = 0;
-#pragma unroll
-  for (int dx = 0; dx < K; ++dx)
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-      if (4 * qd + i < W) bits |= (unsigned long long)(o[(size_t)dx * H * W + i] > 0.f) << (4 * dx + i);
-  mask[t] = bits;
+// out[b * obs + k * HW + p] = epilogue(sum_g part[g][b][k][p] / C), g in order.
+// With the sign mask (zeroed by the split forward kernel before this one
+// runs): each positive activated output ORs its bit 4 dx + x % 4 into word
+// (b, dy, y, x / 4) -- the same words the unsplit forward's epilogue writes.
+__device__ __forceinline__ void mask_or(const FwdEpi& ep, long long i, int KHW, int K, int H, int W) {
+  const int HW = H * W;
+  const long long b = i / KHW;
+  const int r = (int)(i - b * KHW), k = r / HW, pp = r - k * HW;
+  const int dy = k / K, dx = k - dy * K, y = pp / W, x = pp - y * W;
+  atomicOr(ep.mask + ((b * K + dy) * H + y) * ((W + 3) >> 2) + (x >> 2), 1ull << (4 * dx + (x & 3)));
 }
-
-// out[b * obs + k * HW + p] = epilogue(sum_g part[g][b][k][p] / C), g in order
 __global__ __launch_bounds__(256) void corr_fwd_reduce_kernel(const float* __restrict__ part,
                                                               float* __restrict__ out, FwdEpi ep,
-                                                              int G, int B, int KHW, int C) {
+                                                              int G, int B, int KHW, int C, int K,
+                                                              int H, int W) {
   const long long per = (long long)B * KHW;
   const long long i0 = ((long long)blockIdx.x * 256 + threadIdx.x) * 4;
   if (i0 >= per) return;
@@ -489,6 +481,7 @@ __global__ __launch_bounds__(256) void corr_fwd_reduce_kernel(const float* __res
     const float v = s / cf;
     return ep.act ? (v > 0.f ? v : v * ep.slope) : v;
   };
+  const bool bits = ep.act && ep.mask;
   if ((KHW & 3) == 0 && (ep.out_bstride & 3) == 0) {
     float4 s = *reinterpret_cast<const float4*>(part + i0);
     for (int g = 1; g < G; ++g) {
@@ -496,13 +489,22 @@ __global__ __launch_bounds__(256) void corr_fwd_reduce_kernel(const float* __res
       s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
     }
     const long long b = i0 / KHW, r = i0 - b * KHW;
-    *reinterpret_cast<float4*>(out + b * ep.out_bstride + r) = make_float4(fin(s.x), fin(s.y), fin(s.z), fin(s.w));
+    const float4 o = make_float4(fin(s.x), fin(s.y), fin(s.z), fin(s.w));
+    *reinterpret_cast<float4*>(out + b * ep.out_bstride + r) = o;
+    if (bits) {
+      if (o.x > 0.f) mask_or(ep, i0, KHW, K, H, W);
+      if (o.y > 0.f) mask_or(ep, i0 + 1, KHW, K, H, W);
+      if (o.z > 0.f) mask_or(ep, i0 + 2, KHW, K, H, W);
+      if (o.w > 0.f) mask_or(ep, i0 + 3, KHW, K, H, W);
+    }
   } else {
     for (long long i = i0; i < i0 + 4 && i < per; ++i) {
       float s = part[i];
       for (int g = 1; g < G; ++g) s += part[g * per + i];
       const long long b = i / KHW, r = i - b * KHW;
-      out[b * ep.out_bstride + r] = fin(s);
+      const float o = fin(s);
+      out[b * ep.out_bstride + r] = o;
+      if (bits && o > 0.f) mask_or(ep, i, KHW, K, H, W);
     }
   }
 }
@@ -521,19 +523,10 @@ hipError_t launch_fwd_v(const float* x1, const float* x2, float* out, int B, int
     if (e != hipSuccess) return e;
     const int KHW = F::K * F::K * H * W;
     const long long per = (long long)B * KHW;
+    // the element-wise reduce also ORs the sign bits into the mask (a
+    // thread-per-word reduce was 4x slower at L0/L1: 36 x G dependent loads)
     hipLaunchKernelGGL(corr_fwd_reduce_kernel, dim3((unsigned)((per + 1023) / 1024)), dim3(256), 0, s,
-                       ep.part, out, ep, ep.groups, B, KHW, C);
-    if (ep.act && ep.mask) {
-      // a thread-per-word reduce that also writes the mask was measured 4x
-      // slower at L0/L1 (59 vs 15 us: 36 x G dependent partial loads per
-      // thread); the element-wise reduce + this pass keeps the ABI complete,
-      // and the decoder (corr_cat.py) uses the dense derivative at split levels
-      const hipError_t e2 = hipGetLastError();
-      if (e2 != hipSuccess) return e2;
-      const long long n = (long long)B * F::K * H * ((W + 3) / 4);
-      hipLaunchKernelGGL(corr_act_mask_kernel<F::K>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
-                         out, ep.out_bstride, ep.mask, B, H, W);
-    }
+                       ep.part, out, ep, ep.groups, B, KHW, C, F::K, H, W);
   }
   return hipGetLastError();
 }

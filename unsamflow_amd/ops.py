@@ -375,12 +375,11 @@ def _plane_slice_stride(name: str, t: torch.Tensor, shape) -> int:
 def corr_act_mask(B: int, H: int, W: int, max_displacement: int, device, C: int | None = None
                   ) -> torch.Tensor | None:
     """An empty LeakyReLU sign mask for :func:`corr_forward_ex` (int64 words,
-    [B,2d+1,H,ceil(W/4)]). With ``C``: None where the forward splits its channel
-    loop (small levels), whose mask would cost an extra pass over the output --
-    there the backward's dense derivative pass is cheaper."""
+    [B,2d+1,H,ceil(W/4)]), at every level: the unsplit forward writes it in its
+    epilogue, the channel-split forward of the small levels in its reduce.
+    ``C`` is accepted for call-site compatibility (the mask no longer depends
+    on it)."""
     lib = _lib.load()
-    if C is not None and int(lib.usf_corr_fwd_workspace(B, C, H, W, int(max_displacement))) > 0:
-        return None
     n = int(lib.usf_corr_act_mask_words(B, H, W, int(max_displacement)))
     if n == 0:
         return None
