@@ -281,7 +281,9 @@ constexpr int kBinSlots = 4;
 struct BinArgs {
   int* cnt = nullptr;      // [B][(H+1)(W+1)] pixels filed per cell
   int* bins = nullptr;     // [B][(H+1)(W+1)][kBinSlots] source pixel (py << 16 | px)
-  float4* wbin = nullptr;  // [B][(H+1)(W+1)][kBinSlots] its corner weights (nw, ne, sw, se), 0 off-image
+  float* wbin = nullptr;   // [4][B (H+1)(W+1)][kBinSlots] slot weights per corner k (nw, ne, sw, se), 0 off-image:
+                           // a target cell's gather reads one float4 (its 4 slots) per corner
+  long long ncell = 0;     // B (H+1)(W+1)
   int* ovf = nullptr;      // [B * HW] overflow list: b * HW + p
   int* novf = nullptr;     // overflow list length
 };
@@ -322,8 +324,12 @@ __global__ __launch_bounds__(256) void warp_bwd_kernel(const float* __restrict__
       const int slot = atomicAdd(ba.cnt + cell, 1);
       if (slot < kBinSlots) {
         ba.bins[cell * kBinSlots + slot] = (p / W) << 16 | (p % W);  // (py, px): sorts as p
-        ba.wbin[cell * kBinSlots + slot] = make_float4(tp.m_nw ? tp.s * tp.e : 0.f, tp.m_ne ? tp.s * tp.w : 0.f,
-                                                       tp.m_sw ? tp.n * tp.e : 0.f, tp.m_se ? tp.n * tp.w : 0.f);
+        float* wb = ba.wbin + cell * kBinSlots + slot;
+        const size_t ks = (size_t)ba.ncell * kBinSlots;  // corner plane stride
+        wb[0] = tp.m_nw ? tp.s * tp.e : 0.f;
+        wb[ks] = tp.m_ne ? tp.s * tp.w : 0.f;
+        wb[2 * ks] = tp.m_sw ? tp.n * tp.e : 0.f;
+        wb[3 * ks] = tp.m_se ? tp.n * tp.w : 0.f;
       } else {
         ba.ovf[atomicAdd(ba.novf, 1)] = b * HW + p;  // scattered by the overflow pass
       }
@@ -440,13 +446,9 @@ __global__ __launch_bounds__(256) void warp_gx_bins_kernel(const float* __restri
     const size_t ce = valid ? cell : 0;
     const int n = valid ? min(ba.cnt[ce], kBinSlots) : 0;
     const int4 e4 = *reinterpret_cast<const int4*>(ba.bins + ce * kBinSlots);
-    const float4* wb = ba.wbin + ce * kBinSlots;
-    float wv[kBinSlots];
-#pragma unroll
-    for (int j = 0; j < kBinSlots; ++j) {
-      const float4 w4 = (j < 2 || j < n) ? wb[j] : make_float4(0.f, 0.f, 0.f, 0.f);
-      wv[j] = j < n ? (k == 0 ? w4.x : k == 1 ? w4.y : k == 2 ? w4.z : w4.w) : 0.f;
-    }
+    // the 4 slots' weights for this corner: one 16-byte load (corner-major layout)
+    const float4 w4 = *reinterpret_cast<const float4*>(ba.wbin + ((size_t)k * ba.ncell + ce) * kBinSlots);
+    float wv[kBinSlots] = {n > 0 ? w4.x : 0.f, n > 1 ? w4.y : 0.f, n > 2 ? w4.z : 0.f, n > 3 ? w4.w : 0.f};
     pk[k][0] = n > 0 ? e4.x : INT_MAX;
     pk[k][1] = n > 1 ? e4.y : INT_MAX;
     pk[k][2] = n > 2 ? e4.z : INT_MAX;
@@ -486,7 +488,10 @@ __global__ __launch_bounds__(256) void warp_gx_bins_kernel(const float* __restri
     atomicMin(&bb[0], ylo); atomicMax(&bb[1], yhi); atomicMin(&bb[2], xlo); atomicMax(&bb[3], xhi);
   }
   __syncthreads();
-  const int by0 = bb[0], bx0 = bb[2];
+  // box columns start on a 4-float boundary when rows are 16-byte aligned
+  // (W % 4 == 0): every box quad is then one aligned 16-byte load inside its row
+  const bool w4 = (W & 3) == 0;
+  const int by0 = bb[0], bx0 = w4 ? bb[2] & ~3 : bb[2];
   const int bh = bb[1] - by0 + 1, bw = bb[3] - bx0 + 1;
   const bool staged = bb[0] <= bb[1] && bh <= kBoxH && bw <= kBoxW;  // workgroup-uniform
   const float* gb = gout + (size_t)b * C * HW;
@@ -506,28 +511,30 @@ __global__ __launch_bounds__(256) void warp_gx_bins_kernel(const float* __restri
     for (int u = 0; u < kGatherCH; ++u) acc[u] = 0.f;
     if (staged) {
       __syncthreads();  // the previous pass is done with the box
-      // box rows (channel u, row yy) dealt to the 4 waves, lanes along x
-      // (coalesced); every row load of a wave is issued before any store
-      constexpr int kRows = kGatherCH * kBoxH / 4;  // rows per wave, at most
-      constexpr int kHalf = kRows / 2;               // issued together (VGPR budget)
-      const int wv = t >> 6, ln = t & 63;
-      int u = 0, yy = wv;  // row wv + 4 i = u * bh + yy
-      for (int h = 0; h < 2 && u < kGatherCH; ++h) {
-        float v[kHalf];
-        int uu = u, y2 = yy;
+      // thread = (box row t / 16, column quad t % 16): kBoxH x kBoxW = 256 quads,
+      // so each thread stages at most one quad per channel, all loads in flight together
+      static_assert(kBoxH * kBoxW == 4 * 256, "one quad per thread and channel");
+      const int ry = t >> 4, rx = (t & 15) * 4;
+      if (ry < bh && rx < bw) {
+        const float* src = gb + (size_t)(by0 + ry) * W + bx0 + rx;
+        float4 v[kGatherCH];
+        if (w4) {
 #pragma unroll
-        for (int i = 0; i < kHalf; ++i) {
-          while (y2 >= bh) { y2 -= bh; ++uu; }
-          const bool ok = uu < kGatherCH && c + uu < c1 && ln < bw;
-          v[i] = ok ? gb[(size_t)(c + uu) * HW + (by0 + y2) * W + bx0 + ln] : 0.f;
-          y2 += 4;
+          for (int u = 0; u < kGatherCH; ++u)
+            v[u] = c + u < c1 ? *reinterpret_cast<const float4*>(src + (size_t)(c + u) * HW)
+                              : make_float4(0.f, 0.f, 0.f, 0.f);
+        } else {  // unaligned rows: dword loads, none past the row
+          const int nv = min(4, W - (bx0 + rx));
+#pragma unroll
+          for (int u = 0; u < kGatherCH; ++u) {
+            const float* sc = src + (size_t)min(c + u, c1 - 1) * HW;
+            const bool ok = c + u < c1;
+            v[u] = make_float4(ok ? sc[0] : 0.f, ok && nv > 1 ? sc[1] : 0.f, ok && nv > 2 ? sc[2] : 0.f,
+                               ok && nv > 3 ? sc[3] : 0.f);
+          }
         }
 #pragma unroll
-        for (int i = 0; i < kHalf; ++i) {
-          while (yy >= bh) { yy -= bh; ++u; }
-          if (u < kGatherCH) box[u * kBoxCap + yy * kBoxW + ln] = v[i];
-          yy += 4;
-        }
+        for (int u = 0; u < kGatherCH; ++u) *reinterpret_cast<float4*>(&box[u * kBoxCap + ry * kBoxW + rx]) = v[u];
       }
       __syncthreads();
 #pragma unroll
@@ -988,7 +995,8 @@ void bwd_bins(const float* x, const float* flow, long long fbs, const float* gou
   BinArgs ba;
   ba.cnt = reinterpret_cast<int*>(w + L.cnt_off);
   ba.bins = reinterpret_cast<int*>(w + L.bins_off);
-  ba.wbin = reinterpret_cast<float4*>(w + L.wbin_off);
+  ba.wbin = reinterpret_cast<float*>(w + L.wbin_off);
+  ba.ncell = (long long)B * (H + 1) * (W + 1);
   ba.ovf = reinterpret_cast<int*>(w + L.ovf_off);
   ba.novf = reinterpret_cast<int*>(w + L.novf_off);
   (void)hipMemsetAsync(w, 0, (size_t)(L.cnt_off + 4LL * B * (H + 1) * (W + 1)), s);  // novf + counts
