@@ -465,9 +465,9 @@ __global__ __launch_bounds__(256) void warp_gx_bins_kernel(const float* __restri
 #pragma unroll
     for (int j = 0; j < kBinSlots; ++j) {
       const bool has = j < n;
-      const int py = has ? pk[k][j] >> 16 : qy, px = has ? pk[k][j] & 0xFFFF : qx;
+      const int py = pk[k][j] >> 16, px = pk[k][j] & 0xFFFF;
       wk[k][j] = wv[j];
-      pk[k][j] = (py << 16) | px;
+      pk[k][j] = has ? (py << 16) | px : -1;  // empty slot: weight 0 at offset 0 (below)
       if (has) {
         ylo = min(ylo, py); yhi = max(yhi, py); xlo = min(xlo, px); xhi = max(xhi, px);
       }
@@ -501,8 +501,10 @@ __global__ __launch_bounds__(256) void warp_gx_bins_kernel(const float* __restri
   for (int k = 0; k < 4; ++k)
 #pragma unroll
     for (int j = 0; j < kBinSlots; ++j) {
+      // empty slots read element 0 (always staged, finite) with weight 0: the
+      // box is written only where sources lie, so anything else may be stale LDS
       const int py = pk[k][j] >> 16, px = pk[k][j] & 0xFFFF;
-      pk[k][j] = staged ? (py - by0) * kBoxW + (px - bx0) : py * W + px;
+      pk[k][j] = pk[k][j] < 0 ? 0 : staged ? (py - by0) * kBoxW + (px - bx0) : py * W + px;
     }
   // kGatherCH channels per pass with independent accumulators
   for (int c = c0; c < c1; c += kGatherCH) {
@@ -1001,8 +1003,20 @@ void bwd_bins(const float* x, const float* flow, long long fbs, const float* gou
   ba.novf = reinterpret_cast<int*>(w + L.novf_off);
   (void)hipMemsetAsync(w, 0, (size_t)(L.cnt_off + 4LL * B * (H + 1) * (W + 1)), s);  // novf + counts
   // filing pass, with grad_flow's channel slices chosen as for the scatter
-  const long runs64 = (long)B * ((H * W + 63) / 64);
-  const int cs = (runs64 >= 96 && C >= 4) ? 4 : pick_cs(B, C, H * W);
+  // the smallest slice count in {4, 16, 64} that still gives >= 768 workgroups
+  // (profiles/ab_r02/warp_bins_ab.json: L2 31.5 -> 26.7 us with 16 instead of 4;
+  // L3/L4 keep 4, L1 64)
+  int cs = 64;
+  for (const int o : {4, 16}) {
+    if ((long)B * ((H * W + 256 / o - 1) / (256 / o)) >= 768) {
+      cs = o;
+      break;
+    }
+  }
+  while (cs > 4 && cs > C) cs >>= 2;  // no more slices than channels (4 at least)
+#ifdef USF_BIN_CS
+  cs = USF_BIN_CS;  // A/B builds only
+#endif
   switch (cs) {
     case 1: bin_pass_cs<BORDER, 1>(x, flow, fbs, gout, gflow, B, C, H, W, ba, s); break;
     case 4: bin_pass_cs<BORDER, 4>(x, flow, fbs, gout, gflow, B, C, H, W, ba, s); break;
@@ -1014,8 +1028,10 @@ void bwd_bins(const float* x, const float* flow, long long fbs, const float* gou
   const int tiles_x = (W + kBinTW - 1) / kBinTW, ntiles = tiles_x * ((H + kBinTH - 1) / kBinTH);
   const long units = (long)ntiles * B;
   const int chunks = (C + kGatherCH - 1) / kGatherCH;
+// ~1024 workgroups, i.e. >= 16 channels per workgroup wherever the grid
+// allows (L3: 43.3 -> 38.3 us against ~2048; profiles/ab_r02/warp_bins_ab.json)
 #ifndef USF_BIN_WGS
-#define USF_BIN_WGS 2048
+#define USF_BIN_WGS 1024
 #endif
   const int want = (int)std::min<long>(chunks, std::max<long>(1, (USF_BIN_WGS + units - 1) / units));
   const int cper = ((chunks + want - 1) / want) * kGatherCH;
