@@ -271,33 +271,42 @@ struct StageImg {
 };
 
 // ---------------------------------------------------------------- forward --
-template <int D, int PX, int SEGX, int NDY, int CC, int V>
+// CS: channel slices inside one workgroup. With CS > 1 the workgroup has
+// NDY * CS waves; all of them stage each CC-channel stage, and wave group h
+// sums channels [h CC / CS, (h + 1) CC / CS) of it, so the stage buffers are
+// shared (no extra LDS) while CS times as many waves hide the per-channel LDS
+// latency (SURVEY config 2: 1152 waves for 1024 SIMDs at CS = 1). The slices'
+// sums are added through LDS once at the end, in slice order.
+template <int D, int PX, int SEGX, int NDY, int CC, int V, int CS = 1>
 struct FwdCfg {
   static constexpr int K = 2 * D + 1;
   static constexpr int TW = SEGX * PX;              // tile width (pixels)
   static constexpr int TH = 64 / SEGX;              // tile height (rows)
-  static constexpr int NT = 64 * NDY;               // threads per workgroup
+  static constexpr int NW = NDY * CS;               // waves per workgroup
+  static constexpr int NT = 64 * NW;                // threads per workgroup
   static constexpr int NDYG = (K + NDY - 1) / NDY;  // workgroups per tile
   using L = Layout<PX, SEGX, D>;
   static constexpr int R2 = TH + NDY - 1;           // staged x2 rows
   static constexpr int C2 = TW + 2 * D;             // staged x2 cols
   static constexpr int S = L::S;                    // LDS row stride (x1 and x2 images)
-  using X1 = StageImg<TH, TW, S, CC, V, NDY>;        // x1 tile, CC planes
-  using X2 = StageImg<R2, C2, S, CC, V, NDY>;        // x2 halo window, CC planes
+  using X1 = StageImg<TH, TW, S, CC, V, NW>;         // x1 tile, CC planes
+  using X2 = StageImg<R2, C2, S, CC, V, NW>;         // x2 halo window, CC planes
   static constexpr int WIN = round_up(PX + 2 * D, 4);
   static constexpr int STAGE = X1::N + X2::N;
   static constexpr int LDSN = 2 * STAGE + WIN;      // two images + window over-read pad
+  static_assert(CC % CS == 0, "whole channels per slice");
+  static_assert(CS == 1 || 2 * STAGE >= (CS - 1) * NDY * K * PX * 64, "slice sums fit the stage buffers");
   static_assert(PX % 4 == 0, "PX must be a multiple of 4 (ds_read_b128)");
   static_assert(64 % SEGX == 0, "SEGX must divide 64");
   static_assert(V == 1 || L::X4, "16-byte DMA needs the 4-aligned layout");
 };
 
-template <int D, int PX, int SEGX, int NDY, int CC, int V>
-__global__ __launch_bounds__(64 * NDY) void corr_fwd_kernel(const float* __restrict__ x1,
-                                                            const float* __restrict__ x2,
-                                                            float* __restrict__ out, int C,
-                                                            int H, int W, int tiles_x, FwdEpi ep) {
-  using F = FwdCfg<D, PX, SEGX, NDY, CC, V>;
+template <int D, int PX, int SEGX, int NDY, int CC, int V, int CS = 1>
+__global__ __launch_bounds__(64 * NDY * CS) void corr_fwd_kernel(const float* __restrict__ x1,
+                                                                 const float* __restrict__ x2,
+                                                                 float* __restrict__ out, int C,
+                                                                 int H, int W, int tiles_x, FwdEpi ep) {
+  using F = FwdCfg<D, PX, SEGX, NDY, CC, V, CS>;
   constexpr int K = F::K, TW = F::TW, TH = F::TH, S = F::S;
   constexpr int P1 = F::X1::PL, P2 = F::X2::PL, N1 = F::X1::N;
   constexpr int WIN = F::WIN, STAGE = F::STAGE;
@@ -307,7 +316,9 @@ __global__ __launch_bounds__(64 * NDY) void corr_fwd_kernel(const float* __restr
   USF_TRACE_AT(0);
   USF_TRACE_HWID();
   const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wall = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // 0 .. NW-1 (DMA share)
+  const int slice = wall / NDY;                                      // channel slice (uniform)
+  const int wave = wall - slice * NDY;                               // displacement row in the group
   // work item: displacement-row group fastest, then tile, then (sample, channel group)
   const int w = xcd_remap(linear_block(), gridDim.x * gridDim.y * gridDim.z);
   const int dyb = (w % F::NDYG) * NDY;
@@ -329,13 +340,13 @@ __global__ __launch_bounds__(64 * NDY) void corr_fwd_kernel(const float* __restr
   // stage-invariant per-lane DMA offsets (pad columns / off-image pixels: zeros)
   typename F::X1 s1;
   typename F::X2 s2;
-  s1.init(wave, lane, y0, x0, H, W);
-  s2.init(wave, lane, y0 + dyb - D, x0 - D, H, W);
+  s1.init(wall, lane, y0, x0, H, W);
+  s2.init(wall, lane, y0 + dyb - D, x0 - D, H, W);
   const rsrc_t r1 = plane_rsrc(x1 + (size_t)b * C * HW, true, C * HW * 4);
   const rsrc_t r2 = plane_rsrc(x2 + (size_t)b * C * HW, true, C * HW * 4);
   auto dma_stage = [&](int c0, float* img) {
-    s1.load(r1, img, wave, c0, cend, HW);
-    s2.load(r2, img + N1, wave, c0, cend, HW);
+    s1.load(r1, img, wall, c0, cend, HW);
+    s2.load(r2, img + N1, wall, c0, cend, HW);
   };
 
   float acc[K][PX];
@@ -357,7 +368,7 @@ __global__ __launch_bounds__(64 * NDY) void corr_fwd_kernel(const float* __restr
       const float* p1 = cur + r * S + q * PX;
       const float* p2 = cur + N1 + (r + wave) * S + q * PX;
 #pragma unroll 2
-      for (int c = 0; c < CC; ++c) {
+      for (int c = slice * (CC / CS); c < (slice + 1) * (CC / CS); ++c) {
         float a[PX], w[WIN];
         if constexpr (B64 && PX == 8 && WIN == 16) {
           lds_read_px8(p1 + c * P1, p2 + c * P2, a, w);
@@ -384,6 +395,27 @@ __global__ __launch_bounds__(64 * NDY) void corr_fwd_kernel(const float* __restr
     const long long nw = (long long)(gridDim.z / G) * K * H * ((W + 3) >> 2);
     const long long nt = (long long)gridDim.x * gridDim.y * gridDim.z * blockDim.x;
     for (long long i = (long long)linear_block() * blockDim.x + threadIdx.x; i < nw; i += nt) ep.mask[i] = 0ull;
+  }
+  if constexpr (CS > 1) {
+    // slices 1.. hand their sums to slice 0 through the (now idle) stage
+    // buffers; slice 0 adds them in slice order and runs the epilogue
+    float* xa = sm + (wave * K * PX) * 64 + lane;
+    if (slice > 0 && active) {
+#pragma unroll
+      for (int j = 0; j < K; ++j)
+#pragma unroll
+        for (int i = 0; i < PX; ++i) xa[((slice - 1) * NDY * K * PX + j * PX + i) * 64] = acc[j][i];
+    }
+    __syncthreads();
+    if (slice > 0) return;
+    if (active) {
+#pragma unroll
+      for (int h = 1; h < CS; ++h)
+#pragma unroll
+        for (int j = 0; j < K; ++j)
+#pragma unroll
+          for (int i = 0; i < PX; ++i) acc[j][i] += xa[((h - 1) * NDY * K * PX + j * PX + i) * 64];
+    }
   }
   if (!active) return;
   const int y = y0 + r;
@@ -509,14 +541,14 @@ __global__ __launch_bounds__(256) void corr_fwd_reduce_kernel(const float* __res
   }
 }
 
-template <int D, int PX, int SEGX, int NDY, int CC, int V>
+template <int D, int PX, int SEGX, int NDY, int CC, int V, int CS = 1>
 hipError_t launch_fwd_v(const float* x1, const float* x2, float* out, int B, int C, int H, int W,
                         hipStream_t s, FwdEpi ep) {
-  using F = FwdCfg<D, PX, SEGX, NDY, CC, V>;
+  using F = FwdCfg<D, PX, SEGX, NDY, CC, V, CS>;
   const int tiles_x = (W + F::TW - 1) / F::TW;
   const int tiles_y = (H + F::TH - 1) / F::TH;
   dim3 grid(F::NDYG, tiles_x * tiles_y, B * ep.groups);
-  hipLaunchKernelGGL((corr_fwd_kernel<D, PX, SEGX, NDY, CC, V>), grid, dim3(F::NT), 0, s, x1,
+  hipLaunchKernelGGL((corr_fwd_kernel<D, PX, SEGX, NDY, CC, V, CS>), grid, dim3(F::NT), 0, s, x1,
                      x2, out, C, H, W, tiles_x, ep);
   if (ep.groups > 1) {
     const hipError_t e = hipGetLastError();
@@ -532,13 +564,13 @@ hipError_t launch_fwd_v(const float* x1, const float* x2, float* out, int B, int
 }
 
 // 16-byte DMA staging whenever the layout and W allow it (see Layout).
-template <int D, int PX, int SEGX, int NDY, int CC>
+template <int D, int PX, int SEGX, int NDY, int CC, int CS = 1>
 hipError_t launch_fwd(const float* x1, const float* x2, float* out, int B, int C, int H, int W,
                       hipStream_t s, FwdEpi ep) {
   if constexpr (Layout<PX, SEGX, D>::X4) {
-    if (W % 4 == 0) return launch_fwd_v<D, PX, SEGX, NDY, CC, 4>(x1, x2, out, B, C, H, W, s, ep);
+    if (W % 4 == 0) return launch_fwd_v<D, PX, SEGX, NDY, CC, 4, CS>(x1, x2, out, B, C, H, W, s, ep);
   }
-  return launch_fwd_v<D, PX, SEGX, NDY, CC, 1>(x1, x2, out, B, C, H, W, s, ep);
+  return launch_fwd_v<D, PX, SEGX, NDY, CC, 1, CS>(x1, x2, out, B, C, H, W, s, ep);
 }
 
 // Tuning hook: usf_set_variant(0, i) forces candidate i for d=4
@@ -554,10 +586,14 @@ hipError_t fwd_candidate_d4(int i, const float* x1, const float* x2, float* out,
     case 5: return launch_fwd<4, 4, 8, 3, 4>(x1, x2, out, B, C, H, W, s, ep);
     case 6: return launch_fwd<4, 8, 8, 3, 4>(x1, x2, out, B, C, H, W, s, ep);
     case 7: return launch_fwd<4, 4, 8, 1, 8>(x1, x2, out, B, C, H, W, s, ep);
+    case 8: return launch_fwd<4, 4, 8, 3, 8, 2>(x1, x2, out, B, C, H, W, s, ep);
+    case 9: return launch_fwd<4, 4, 8, 3, 4, 2>(x1, x2, out, B, C, H, W, s, ep);
+    case 10: return launch_fwd<4, 4, 8, 1, 8, 2>(x1, x2, out, B, C, H, W, s, ep);
+    case 11: return launch_fwd<4, 4, 8, 1, 8, 4>(x1, x2, out, B, C, H, W, s, ep);
     default: return hipErrorInvalidValue;
   }
 }
-constexpr int kFwdCandidates = 8;
+constexpr int kFwdCandidates = 12;
 
 // Shape heuristic: all displacement rows in one workgroup (x1/x2 staged once)
 // when that still fills the 256 CUs; else split displacement rows across
@@ -612,8 +648,13 @@ hipError_t fwd_dispatch(const float* x1, const float* x2, float* out, int B, int
   if (p.groups > 1 && ws && ws_floats >= need) {
     ep.part = ws;
     ep.groups = p.groups;
+    return launch_fwd<D, 4, 8, 3, 8>(x1, x2, out, B, C, H, W, s, ep);
   }
-  return launch_fwd<D, 4, 8, 3, 8>(x1, x2, out, B, C, H, W, s, ep);
+  // unsplit mid-size grids: two channel slices per workgroup on shared stages
+  // (profiles/ab_r02/fwd_slices.json: KITTI L2 18.3 -> 14.6 us, SURVEY config 1
+  // 9.3 -> 8.2 us with CC = 8; config 2 (C = 128) 25.7 -> 24.4 us with CC = 4)
+  if (C >= 128) return launch_fwd<D, 4, 8, 3, 4, 2>(x1, x2, out, B, C, H, W, s, ep);
+  return launch_fwd<D, 4, 8, 3, 8, 2>(x1, x2, out, B, C, H, W, s, ep);
 }
 
 // --------------------------------------------------------------- backward --
