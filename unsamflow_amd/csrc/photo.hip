@@ -128,8 +128,11 @@ __device__ __forceinline__ void stage_load(Px& p, const float* __restrict__ srcb
 }
 
 // masks applied after the loads landed; rec in ATen's order; x, y to LDS
-__device__ __forceinline__ void stage_finish(Px& p, int C, float (*xs)[kRH][kXS],
-                                             float (*ys)[kRH][kXS], int ry, int rx,
+// (x, y) of one region pixel: one 8-byte LDS slot, so a window row's six
+// values are three ds_read_b64 and the window statistics run on packed pairs
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ void stage_finish(Px& p, int C, f2 (*xy)[kRH][kXS], int ry, int rx,
                                              float (&rec)[kMaxC]) {
 #pragma clang fp contract(off)
   const Tap& tp = p.tp;
@@ -142,8 +145,7 @@ __device__ __forceinline__ void stage_finish(Px& p, int C, float (*xs)[kRH][kXS]
     p.v[c][2] = tp.m_sw ? p.v[c][2] : 0.f;
     p.v[c][3] = tp.m_se ? p.v[c][3] : 0.f;
     rec[c] = p.v[c][0] * wnw + p.v[c][1] * wne + p.v[c][2] * wsw + p.v[c][3] * wse;
-    xs[c][ry][rx] = p.in ? rec[c] * p.m : 0.f;
-    ys[c][ry][rx] = p.in ? p.t[c] * p.m : 0.f;
+    xy[c][ry][rx] = f2{p.in ? rec[c] * p.m : 0.f, p.in ? p.t[c] * p.m : 0.f};
   }
 }
 
@@ -176,18 +178,18 @@ __device__ __forceinline__ void block_sum3(float a, float b, float c, float* red
   }
 }
 
-// sums over 3 columns of one region row: {x, y, x^2, y^2, xy}
+// sums over 3 columns of one region row: {x, y}, {x^2, y^2}, xy (the pairs
+// as packed fp32: the same per-component operations as the scalar forms)
 struct Row5 {
-  float sx, sy, sxx, syy, sxy;
+  f2 s, ss;
+  float sxy;
 };
-__device__ __forceinline__ Row5 row5(const float* xr, const float* yr) {
+__device__ __forceinline__ Row5 row5(const f2* r3) {
   Row5 r;
-  const float a0 = xr[0], a1 = xr[1], a2 = xr[2], b0 = yr[0], b1 = yr[1], b2 = yr[2];
-  r.sx = a0 + a1 + a2;
-  r.sy = b0 + b1 + b2;
-  r.sxx = fmaf(a2, a2, fmaf(a1, a1, a0 * a0));
-  r.syy = fmaf(b2, b2, fmaf(b1, b1, b0 * b0));
-  r.sxy = fmaf(a2, b2, fmaf(a1, b1, a0 * b0));
+  const f2 v0 = r3[0], v1 = r3[1], v2 = r3[2];
+  r.s = v0 + v1 + v2;
+  r.ss = __builtin_elementwise_fma(v2, v2, __builtin_elementwise_fma(v1, v1, v0 * v0));
+  r.sxy = fmaf(v2.x, v2.y, fmaf(v1.x, v1.y, v0.x * v0.y));
   return r;
 }
 
@@ -200,12 +202,15 @@ template <bool GRAD>
 __device__ __forceinline__ float ssim_window(const Row5& r0, const Row5& r1, const Row5& r2,
                                              float& al, float& be, float& ga) {
   constexpr float k9 = 1.0f / 9.0f;
-  const float mx = (r0.sx + r1.sx + r2.sx) * k9, my = (r0.sy + r1.sy + r2.sy) * k9;
-  const float exx = (r0.sxx + r1.sxx + r2.sxx) * k9, eyy = (r0.syy + r1.syy + r2.syy) * k9;
+  const f2 m = (r0.s + r1.s + r2.s) * k9;     // mx, my
+  const f2 e = (r0.ss + r1.ss + r2.ss) * k9;  // exx, eyy
+  const float mx = m.x, my = m.y;
   const float exy = (r0.sxy + r1.sxy + r2.sxy) * k9;
-  const float mxy = mx * my, mx2 = mx * mx, my2 = my * my;
+  const float mxy = mx * my;
+  const f2 m2 = m * m;   // mx^2, my^2
+  const f2 sg = e - m2;  // sig_x, sig_y
   const float A1 = 2.f * mxy + kC1, A2 = 2.f * (exy - mxy) + kC2;
-  const float B1 = mx2 + my2 + kC1, B2 = (exx - mx2) + (eyy - my2) + kC2;
+  const float B1 = m2.x + m2.y + kC1, B2 = sg.x + sg.y + kC2;
   const float d = B1 * B2;
   const float rd = __builtin_amdgcn_rcpf(d);
   const float r = (A1 * A2) * rd;
@@ -227,7 +232,7 @@ __device__ __forceinline__ float ssim_window(const Row5& r0, const Row5& r1, con
 // halos and gather footprints) of one sample run on one L2
 template <bool BORDER, bool GRAD>
 __global__ __launch_bounds__(kNT) void photo_fwd_kernel(PhotoArgs a, float* __restrict__ partials) {
-  __shared__ float xs[kMaxC][kRH][kXS], ys[kMaxC][kRH][kXS];
+  __shared__ f2 xy[kMaxC][kRH][kXS];
   __shared__ float al[GRAD ? kMaxC : 1][GRAD ? kWH : 1][GRAD ? kAS : 1];
   __shared__ float be[GRAD ? kMaxC : 1][GRAD ? kWH : 1][GRAD ? kAS : 1];
   __shared__ float ga[GRAD ? kMaxC : 1][GRAD ? kWH : 1][GRAD ? kAS : 1];
@@ -263,7 +268,7 @@ __global__ __launch_bounds__(kNT) void photo_fwd_kernel(PhotoArgs a, float* __re
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
     float rec[kMaxC];
-    stage_finish(own[k], C, xs, ys, ly0 + k + 2, lx + 2, rec);
+    stage_finish(own[k], C, xy, ly0 + k + 2, lx + 2, rec);
     const Px& p = own[k];
     if (p.in) msum += p.m;
 #pragma unroll
@@ -281,7 +286,7 @@ __global__ __launch_bounds__(kNT) void photo_fwd_kernel(PhotoArgs a, float* __re
   }
   if (has_halo) {
     float rec[kMaxC];
-    stage_finish(hp, C, xs, ys, hy, hx, rec);
+    stage_finish(hp, C, xy, hy, hx, rec);
   }
   __syncthreads();
 
@@ -301,7 +306,7 @@ __global__ __launch_bounds__(kNT) void photo_fwd_kernel(PhotoArgs a, float* __re
         if (c >= C) break;
         Row5 rs[kWG + 2];
 #pragma unroll
-        for (int i = 0; i < kWG + 2; ++i) rs[i] = row5(&xs[c][wy0 + i][wx], &ys[c][wy0 + i][wx]);
+        for (int i = 0; i < kWG + 2; ++i) rs[i] = row5(&xy[c][wy0 + i][wx]);
 #pragma unroll
         for (int r = 0; r < kWG; ++r) {
           const int wy = wy0 + r, qy = ty0 - 2 + wy;
@@ -343,7 +348,8 @@ __global__ __launch_bounds__(kNT) void photo_fwd_kernel(PhotoArgs a, float* __re
       const float sa = ra[k] + ra[k + 1] + ra[k + 2];
       const float sb = rb[k] + rb[k + 1] + rb[k + 2];
       const float sgm = rg[k] + rg[k + 1] + rg[k + 2];
-      const float xp = xs[c][ly0 + k + 2][lx + 2], yp = ys[c][ly0 + k + 2][lx + 2];
+      const f2 pxy = xy[c][ly0 + k + 2][lx + 2];
+      const float xp = pxy.x, yp = pxy.y;
       const float ds = sa + sb * xp + sgm * yp;  // sum_q dS_q / dx_pc
       ax[k] += sg[k][c] * dix[k][c];
       ay[k] += sg[k][c] * diy[k][c];
