@@ -22,7 +22,13 @@ def flows(B, H, W, dev, g):
     xx = torch.linspace(0, 6.2832, W, device=dev).view(1, 1, 1, W)
     ph = torch.rand(B, 2, 1, 1, device=dev, generator=g) * 6.2832
     base = (torch.sin(2 * xx + ph) + torch.cos(3 * yy - ph)).contiguous()
-    return {"zero": torch.zeros(B, 2, H, W, device=dev), "pm2": base, "pm8": (4 * base).contiguous()}
+    # shift: a large smooth motion (about 1/8 of the width plus the +-2 px field,
+    # so a border strip maps outside the image and clamps onto the edge cells)
+    shift = base.clone()
+    shift[:, 0] += W / 8.0
+    shift[:, 1] -= H / 16.0
+    return {"zero": torch.zeros(B, 2, H, W, device=dev), "pm2": base, "pm8": (4 * base).contiguous(),
+            "shift": shift.contiguous()}
 
 
 def main():

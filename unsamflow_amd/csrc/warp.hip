@@ -570,28 +570,66 @@ __global__ __launch_bounds__(256) void warp_gx_bins_kernel(const float* __restri
 }
 
 // Overflow pixels of the binned grad_x add their four corner contributions
-// with float atomics after the gather pass (thread = list entry x channel;
-// the loop bound is the device-side list length, so the kernel exits at once
-// when nothing overflowed).
+// with float atomics after the gather pass. A wave takes 64 consecutive list
+// entries (lane = entry) x kOvfCh channels: consecutive entries mostly share
+// their cell (the list fills in pixel order, and a border-clamped strip piles
+// onto one edge cell per row), so runs of lanes with the same cell are summed
+// by a segmented shuffle scan (row_runs / run_sum, as the scatter does) and
+// only run tails issue the atomics. With one atomic per (entry, channel,
+// corner) the large-shift field took 111 us at L4 on same-address atomics.
+// The loop bound is the device-side list length: nothing overflowed, nothing runs.
+constexpr int kOvfCh = 4;
 template <bool BORDER>
 __global__ __launch_bounds__(256) void warp_gx_ovf_kernel(const float* __restrict__ flow, long long fbs,
                                                           const float* __restrict__ gout, BinArgs ba,
                                                           float* __restrict__ gx, int C, int H, int W) {
   const int HW = H * W;
-  const long long total = (long long)(*ba.novf) * C;
-  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
-    const int ent = ba.ovf[i / C];
-    const int c = (int)(i % C);
+  const int n = *ba.novf;
+  const int lane = threadIdx.x & 63;
+  const int ngrp = (C + kOvfCh - 1) / kOvfCh;
+  const long long units = (long long)((n + 63) / 64) * ngrp;  // (64-entry chunk, channel group)
+  const long long nw = (long long)gridDim.x * (blockDim.x >> 6);
+  for (long long u = (long long)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); u < units; u += nw) {
+    const int chunk = (int)(u / ngrp), grp = (int)(u - (long long)chunk * ngrp);
+    const int e = chunk * 64 + lane;
+    const bool valid = e < n;
+    const int ent = valid ? ba.ovf[e] : 0;
     const int b = ent / HW, p = ent - b * HW;
     const int y = p / W, xx = p - y * W;
     const float* fb = flow + b * fbs;
-    const Tap tp = make_tap(fb[p], fb[HW + p], xx, y, H, W, BORDER);
-    const float go = gout[((size_t)b * C + c) * HW + p];
-    float* gc = gx + ((size_t)b * C + c) * HW;
-    if (tp.m_nw) atomicAdd(gc + tp.o_nw, go * (tp.s * tp.e));
-    if (tp.m_ne) atomicAdd(gc + tp.o_ne, go * (tp.s * tp.w));
-    if (tp.m_sw) atomicAdd(gc + tp.o_sw, go * (tp.n * tp.e));
-    if (tp.m_se) atomicAdd(gc + tp.o_se, go * (tp.n * tp.w));
+    Tap tp = make_tap(fb[p], fb[HW + p], xx, y, H, W, BORDER);
+    if (!valid) tp.m_nw = tp.m_ne = tp.m_sw = tp.m_se = false;
+    // run key: the entry's north-west cell (same cell = same four corners and masks)
+    const bool any = tp.m_nw || tp.m_ne || tp.m_sw || tp.m_se;
+    const int key = any ? (int)(((long long)b * (H + 1) + tp.yn + 1) * (W + 1) + tp.xw + 1) : -(lane + 2);
+    const int kl = __shfl_up(key, 1);
+    const bool head = lane == 0 || kl != key;
+    const unsigned long long heads = __ballot(head);
+    const unsigned long long upto = lane == 63 ? ~0ull : ((2ull << lane) - 1);
+    RowRuns r;
+    r.pos = lane - (63 - __clzll(heads & upto));
+    r.tail = lane == 63 || ((heads >> (lane + 1)) & 1ull) != 0;
+    int m = r.pos;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = max(m, __shfl_xor(m, o));
+    r.maxlen = m + 1;
+    const float wv[4] = {tp.s * tp.e, tp.s * tp.w, tp.n * tp.e, tp.n * tp.w};
+    const bool mk[4] = {tp.m_nw, tp.m_ne, tp.m_sw, tp.m_se};
+    const int ok[4] = {tp.o_nw, tp.o_ne, tp.o_sw, tp.o_se};
+    const int c0 = grp * kOvfCh;
+    float go[kOvfCh];  // all of the group's loads in flight together
+#pragma unroll
+    for (int j = 0; j < kOvfCh; ++j)
+      go[j] = valid && c0 + j < C ? gout[((size_t)b * C + c0 + j) * HW + p] : 0.f;
+#pragma unroll
+    for (int j = 0; j < kOvfCh; ++j) {
+      const size_t bs = ((size_t)b * C + c0 + j) * HW;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float v = run_sum(go[j] * wv[k], r);  // every lane takes part (shuffles)
+        if (r.tail && mk[k] && c0 + j < C) atomicAdd(gx + bs + ok[k], v);
+      }
+    }
   }
 }
 
