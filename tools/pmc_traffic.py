@@ -67,14 +67,17 @@ def main():
     lib = _lib.load()  # host-only query: split forwards run a second (reduce) kernel
     for op, key in selected_sites():
         k = per_launch.get(op, 1)
-        if op == "corr_fwd" and lib.usf_corr_fwd_workspace(*key[:4], 4) > 0:
+        split = lib.usf_corr_fwd_workspace(*key[:4], 4) > 0 if op.startswith("corr") else False
+        if op == "corr_fwd" and split:
             k = 2
         pos += prefix.get(op, 0)
-        if op == "corr_bwd_leaky" and lib.usf_corr_fwd_workspace(*key[:4], 4) == 0:
-            # sign-mask path (unsplit forward): one backward kernel per launch,
-            # after the launcher's one forward kernel
+        if op == "corr_bwd_leaky":
+            # sign-mask path at every level: one backward kernel per launch, after
+            # the launcher's forward (two kernels where the forward is split)
             k = 1
-            pos += 1
+            pos += 2 if split else 1
+        if op == "warp_bwd" and key[5]:
+            k = 3  # binned grad_x: filing (+ grad_flow), gather, overflow
         fk = statistics.median(sum(uf[pos + j * k + i] for i in range(k)) for j in range(n))
         wk = statistics.median(sum(uw[pos + j * k + i] for i in range(k)) for j in range(n))
         pos += k * n
@@ -87,9 +90,8 @@ def main():
         if op.startswith("corr"):
             alg = corr_bytes(*key[:4], backward=op.startswith("corr_bwd"))
             if op == "corr_bwd_leaky":
-                words = lib.usf_corr_act_mask_words(B, H, W, 4) if lib.usf_corr_fwd_workspace(B, C, H, W, 4) == 0 else 0
-                # the derivative's input: the sign mask, else the activated output
-                alg += 8 * words if words else 4 * B * H * W * 81
+                # the derivative's input: the forward's sign mask
+                alg += 8 * lib.usf_corr_act_mask_words(B, H, W, 4)
         elif op == "convex_up":
             alg = 4 * B * H * W * (2 + 11 * f * f)
         elif op == "convex_up_bwd":
