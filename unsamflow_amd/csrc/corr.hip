@@ -1004,6 +1004,18 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(USF_BWD
   // they cut the FETCH traffic (2.6x -> 1.4x of algorithmic). Short chunks
   // (below) keep both.
   int w = linear_block();
+#ifndef USF_BWD_DIRFAST
+#define USF_BWD_DIRFAST 1
+#endif
+#ifndef USF_BWD_DIRFAST_CHUNK
+#define USF_BWD_DIRFAST_CHUNK 28
+#endif
+  // direction fastest (MODE 3, chunked levels): a tile's gx1 and gx2 items are
+  // neighbours in one XCD chunk (same L2, same time), so the second read of
+  // its g slice hits L2. Measured at L4, batch 16 (profiles/ab_r02/bwd_dirfast_pmc.json):
+  // FETCH 215.6 -> 157.9 MB per launch (traffic 1.48x -> 1.16x of algorithmic)
+  // at the same time (69.9 vs 67.8 us): this kernel is not HBM-bound.
+  const bool dirfast = MODE == 3 && USF_BWD_DIRFAST && USF_BWD_CHUNK > 0 && gridDim.x >= 16;
   if (USF_BWD_CHUNK > 0 && gridDim.x >= 16) {
     // Q consecutive work items per XCD, chunks dealt round-robin over the 8
     // XCDs (block lin runs on XCD lin % 8; it gets item Q (8 m + x) + j): a few
@@ -1011,17 +1023,10 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(USF_BWD
     // gets a mix of samples and directions. L4 59.5 -> 54.5 us, L3 43 -> 40 us
     // (profiles/ab_r01/bwd_chunk_*.json); whole-sample chunks (xcd_remap) are
     // slower (84 us) and so are levels with < 16 tiles (L1 11.6 -> 13.5 us).
-    w = xcd_chunk(w, gridDim.x * gridDim.y * gridDim.z, USF_BWD_CHUNK);
+    w = xcd_chunk(w, gridDim.x * gridDim.y * gridDim.z, dirfast ? USF_BWD_DIRFAST_CHUNK : USF_BWD_CHUNK);
   }
-#ifndef USF_BWD_DIRFAST
-#define USF_BWD_DIRFAST 0
-#endif
   int group, tile, b;
-  if (MODE == 3 && USF_BWD_DIRFAST) {
-    // direction fastest: a tile's gx1 and gx2 items are neighbours in the
-    // chunk (same XCD, same time), so the second read of its g slice can hit L2.
-    // Measured at batch 16 (profiles/ab_r01/bwd_dirfast.json): no change
-    // (L4 74.4 vs 75.4 us; 72.6 with 28-item chunks), so off by default.
+  if (dirfast) {
     const int dir = w & 1, w2 = w >> 1;
     group = w2 % gridDim.y;
     tile = (w2 / gridDim.y) % gridDim.x;
