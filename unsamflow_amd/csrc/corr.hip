@@ -1005,7 +1005,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(USF_BWD
   // (below) keep both.
   int w = linear_block();
 #ifndef USF_BWD_DIRFAST
-#define USF_BWD_DIRFAST 1
+#define USF_BWD_DIRFAST 0
 #endif
 #ifndef USF_BWD_DIRFAST_CHUNK
 #define USF_BWD_DIRFAST_CHUNK 28
@@ -1014,7 +1014,8 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(USF_BWD
   // neighbours in one XCD chunk (same L2, same time), so the second read of
   // its g slice hits L2. Measured at L4, batch 16 (profiles/ab_r02/bwd_dirfast_pmc.json):
   // FETCH 215.6 -> 157.9 MB per launch (traffic 1.48x -> 1.16x of algorithmic)
-  // at the same time (69.9 vs 67.8 us): this kernel is not HBM-bound.
+  // at the same replayed time (69.9 vs 67.8 us), but 6 us slower inside the
+  // training step (rocprof: 75.7 vs 69.6 us, profiles/r02_v3_*): off by default.
   const bool dirfast = MODE == 3 && USF_BWD_DIRFAST && USF_BWD_CHUNK > 0 && gridDim.x >= 16;
   if (USF_BWD_CHUNK > 0 && gridDim.x >= 16) {
     // Q consecutive work items per XCD, chunks dealt round-robin over the 8
