@@ -286,6 +286,7 @@ struct BinArgs {
   long long ncell = 0;     // B (H+1)(W+1)
   int* ovf = nullptr;      // [B * HW] overflow list: b * HW + p
   int* novf = nullptr;     // overflow list length
+  int ovf_cap = 0;         // list capacity (B * HW): a pixel is listed at most once per call
 };
 
 template <bool BORDER, bool WANT_GX, bool WANT_GF, int CS, int OUTL = 0, bool BIN = false>
@@ -331,7 +332,10 @@ __global__ __launch_bounds__(256) void warp_bwd_kernel(const float* __restrict__
         wb[2 * ks] = tp.m_sw ? tp.n * tp.e : 0.f;
         wb[3 * ks] = tp.m_se ? tp.n * tp.w : 0.f;
       } else {
-        ba.ovf[atomicAdd(ba.novf, 1)] = b * HW + p;  // scattered by the overflow pass
+        // scattered by the overflow pass; the capacity test only matters if the
+        // per-call zero fill of novf / counts did not run (every pixel lists once)
+        const int o = atomicAdd(ba.novf, 1);
+        if (o < ba.ovf_cap) ba.ovf[o] = b * HW + p;
       }
     }
   }
@@ -584,7 +588,7 @@ __global__ __launch_bounds__(256) void warp_gx_ovf_kernel(const float* __restric
                                                           const float* __restrict__ gout, BinArgs ba,
                                                           float* __restrict__ gx, int C, int H, int W) {
   const int HW = H * W;
-  const int n = *ba.novf;
+  const int n = min(*ba.novf, ba.ovf_cap);
   const int lane = threadIdx.x & 63;
   const int ngrp = (C + kOvfCh - 1) / kOvfCh;
   const long long units = (long long)((n + 63) / 64) * ngrp;  // (64-entry chunk, channel group)
@@ -1039,6 +1043,7 @@ void bwd_bins(const float* x, const float* flow, long long fbs, const float* gou
   ba.ncell = (long long)B * (H + 1) * (W + 1);
   ba.ovf = reinterpret_cast<int*>(w + L.ovf_off);
   ba.novf = reinterpret_cast<int*>(w + L.novf_off);
+  ba.ovf_cap = B * H * W;
   (void)hipMemsetAsync(w, 0, (size_t)(L.cnt_off + 4LL * B * (H + 1) * (W + 1)), s);  // novf + counts
   // filing pass, with grad_flow's channel slices chosen as for the scatter
   // the smallest slice count in {4, 16, 64} that still gives >= 768 workgroups
