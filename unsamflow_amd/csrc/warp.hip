@@ -1002,6 +1002,31 @@ void bwd_gather_cs(const float* x, const float* flow, long long fbs, const float
 
 // Binned-gather workspace: overflow count and cell counts (zeroed per call),
 // cell slots with their weights, overflow list.
+// Zero fill as a kernel on the launch stream. Under stream capture a
+// hipMemsetAsync here raced the kernel launched after it on graph replay (the
+// binned backward's cell counts were still stale when the filing pass began:
+// tests/test_gpu_graph_replay.py), so every fill the library needs is this
+// launch, ordered like its other kernels in eager and captured streams alike.
+// p 16-byte aligned (torch allocations, the workspace layout), bytes % 4 == 0.
+__global__ __launch_bounds__(256) void zero_fill_kernel(unsigned* __restrict__ p, long long n) {
+  const long long stride = (long long)gridDim.x * 256 * 4;
+  for (long long i = ((long long)blockIdx.x * 256 + threadIdx.x) * 4; i < n; i += stride) {
+    if (i + 4 <= n) {
+      *reinterpret_cast<uint4*>(p + i) = make_uint4(0u, 0u, 0u, 0u);
+    } else {
+      for (long long j = i; j < n; ++j) p[j] = 0u;
+    }
+  }
+}
+
+hipError_t zero_fill(void* p, size_t bytes, hipStream_t s) {
+  const long long n = (long long)(bytes / 4);
+  if (n <= 0) return hipSuccess;
+  const long long blocks = std::min<long long>((n + 1023) / 1024, 4096);
+  hipLaunchKernelGGL(zero_fill_kernel, dim3((unsigned)blocks), dim3(256), 0, s, static_cast<unsigned*>(p), n);
+  return hipGetLastError();
+}
+
 struct BinLayout {
   long long novf_off, cnt_off, bins_off, wbin_off, ovf_off, total;
 };
@@ -1044,7 +1069,7 @@ void bwd_bins(const float* x, const float* flow, long long fbs, const float* gou
   ba.ovf = reinterpret_cast<int*>(w + L.ovf_off);
   ba.novf = reinterpret_cast<int*>(w + L.novf_off);
   ba.ovf_cap = B * H * W;
-  (void)hipMemsetAsync(w, 0, (size_t)(L.cnt_off + 4LL * B * (H + 1) * (W + 1)), s);  // novf + counts
+  (void)zero_fill(w, (size_t)(L.cnt_off + 4LL * B * (H + 1) * (W + 1)), s);  // novf + counts
   // filing pass, with grad_flow's channel slices chosen as for the scatter
   // the smallest slice count in {4, 16, 64} that still gives >= 768 workgroups
   // (profiles/ab_r02/warp_bins_ab.json: L2 31.5 -> 26.7 us with 16 instead of 4;
@@ -1116,7 +1141,7 @@ void bwd_launch_pad(const float* x, const float* flow, long long fbs, const floa
     return;
   }
   // the scatter variants accumulate into gx: zero it first (gx is overwritten either way)
-  if (gx) (void)hipMemsetAsync(gx, 0, sizeof(float) * (size_t)B * C * H * W, s);
+  if (gx) (void)zero_fill(gx, sizeof(float) * (size_t)B * C * H * W, s);
   // pixel-pair scatter: variant 5, and the default for large levels. Measured at
   // batch 16 (profiles/ab_r01/warp_pairs.json, grad_x + grad_flow): L4 67 vs
   // 82 us (zero flow), 50 vs 60 (constant sub-pixel), equal for +-2 / +-8 px
@@ -1318,7 +1343,7 @@ long long warp_bwd_workspace(int B, int H, int W) { return bin_layout(B, H, W).t
 
 hipError_t splat_launch(const float* flow, long long fbs, float* map, int B, int H, int W,
                         bool absolute, hipStream_t s) {
-  hipError_t e = hipMemsetAsync(map, 0, (size_t)B * H * W * sizeof(float), s);
+  hipError_t e = zero_fill(map, (size_t)B * H * W * sizeof(float), s);
   if (e != hipSuccess) return e;
   const long pairs = (long)W * ((H + 1) / 2);
   if (pairs >= 4096 && variant_override(2) != 0) {  // pixel pairs (as the warp backward)
