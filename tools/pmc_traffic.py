@@ -56,8 +56,8 @@ def main():
     f_read, f_write = calib(fetch), calib(write)
     uf = [v for name, v in fetch if "usf::" in name]
     uw = [v for name, v in write if "usf::" in name]
-    # library kernels per launch of a site (summed): splat + threshold, partials + final
-    per_launch = {"occ_bwd": 2, "photo_fwd": 2, "photo_fwd_grad": 2, "photo_pair_grad": 2, "corr_bwd_leaky": 2,
+    # library kernels per launch of a site (summed): zero fill + splat + threshold, partials + final
+    per_launch = {"occ_bwd": 3, "photo_fwd": 2, "photo_fwd_grad": 2, "photo_pair_grad": 2, "corr_bwd_leaky": 2,
                   "convex_up_bwd": 2}
     # kernels a site's launcher runs once before its timed launches
     prefix = {}
@@ -77,7 +77,7 @@ def main():
             k = 1
             pos += 2 if split else 1
         if op == "warp_bwd" and key[5]:
-            k = 3  # binned grad_x: filing (+ grad_flow), gather, overflow
+            k = 4  # binned grad_x: zero fill, filing (+ grad_flow), gather, overflow
         fk = statistics.median(sum(uf[pos + j * k + i] for i in range(k)) for j in range(n))
         wk = statistics.median(sum(uw[pos + j * k + i] for i in range(k)) for j in range(n))
         pos += k * n
