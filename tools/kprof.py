@@ -16,6 +16,7 @@ from unsamflow_amd.kernel_timer import site_launcher  # noqa: E402
 KITTI = [(192, 4, 13), (128, 8, 26), (96, 16, 52), (64, 32, 104), (32, 64, 208)]
 DB = int(os.environ.get("KPROF_DECODER_B", "16"))  # decoder batch: 2 x 8 pairs
 SITES = [("corr_fwd", (DB, C, H, W)) for C, H, W in KITTI]
+SITES += [("corr_fwd_leaky", (DB, C, H, W)) for C, H, W in KITTI]
 SITES += [("corr_bwd", (DB, C, H, W, True, True)) for C, H, W in KITTI]
 # one direction at a time (where the backward's traffic comes from)
 SITES += [("corr_bwd", (DB, C, H, W, n1, not n1)) for C, H, W in KITTI[3:] for n1 in (True, False)]

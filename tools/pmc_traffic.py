@@ -68,7 +68,7 @@ def main():
     for op, key in selected_sites():
         k = per_launch.get(op, 1)
         split = lib.usf_corr_fwd_workspace(*key[:4], 4) > 0 if op.startswith("corr") else False
-        if op == "corr_fwd" and split:
+        if op in ("corr_fwd", "corr_fwd_leaky") and split:
             k = 2
         pos += prefix.get(op, 0)
         if op == "corr_bwd_leaky":
@@ -89,8 +89,8 @@ def main():
             B, C, H, W = key[:4]
         if op.startswith("corr"):
             alg = corr_bytes(*key[:4], backward=op.startswith("corr_bwd"))
-            if op == "corr_bwd_leaky":
-                # the derivative's input: the forward's sign mask
+            if op in ("corr_bwd_leaky", "corr_fwd_leaky"):
+                # the sign mask: written by the decoder's forward, read by its backward
                 alg += 8 * lib.usf_corr_act_mask_words(B, H, W, 4)
         elif op == "convex_up":
             alg = 4 * B * H * W * (2 + 11 * f * f)

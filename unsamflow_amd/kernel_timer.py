@@ -159,6 +159,13 @@ def site_launcher(op: str, key, device, seed: int = 0):
             ops.corr_forward_ex(x1, x2, 4, act[:, :81], 0.1, act_mask=mask)
         return lambda: ops.corr_backward_ex(x1, x2, cat[:, :81], 4, key[4], key[5], act_out=act[:, :81],
                                             act_mask=mask)
+    if op == "corr_fwd_leaky":  # the decoder's forward: LeakyReLU into a concat slice + sign mask
+        B, C, H, W = key[:4]
+        x1 = torch.randn(B, C, H, W, device=device, generator=g)
+        x2 = torch.randn(B, C, H, W, device=device, generator=g)
+        cat = torch.empty(B, 81 + C + 2, H, W, device=device)
+        mask = ops.corr_act_mask(B, H, W, 4, device, C=C)
+        return lambda: ops.corr_forward_ex(x1, x2, 4, cat[:, :81], 0.1, act_mask=mask)
     if op in ("corr_fwd", "corr_bwd"):
         B, C, H, W = key[:4]
         x1 = torch.randn(B, C, H, W, device=device, generator=g)

@@ -410,8 +410,12 @@ def corr_forward_ex(x1: torch.Tensor, x2: torch.Tensor, max_displacement: int, o
                 or act_mask.numel() != int(lib.usf_corr_act_mask_words(B, H, W, d)):
             raise ValueError("act_mask: a contiguous int64 corr_act_mask() tensor with leaky_slope set")
     ws, nws = _corr_workspace(lib, B, C, H, W, d, x1.device)
+    # the decoder's site (LeakyReLU epilogue into the concat slice, + the sign mask)
+    # is its own timing site, so its device time is measured on the same call
+    op = "corr_fwd_leaky" if act else "corr_fwd"
+    nbytes = _kt.corr_bytes(B, C, H, W, K * K) + (8 * act_mask.numel() if act_mask is not None else 0)
     with torch.cuda.device(x1.device), _kt.timed(
-        "corr_fwd", (B, C, H, W), x1.device, _kt.corr_bytes(B, C, H, W, K * K), _kt.corr_flops(B, C, H, W, K * K)
+        op, (B, C, H, W), x1.device, nbytes, _kt.corr_flops(B, C, H, W, K * K)
     ):
         rc = lib.usf_corr_fwd_ex_f32(x1c.data_ptr(), x2c.data_ptr(), out.data_ptr(), obs, act,
                                      float(leaky_slope or 0.0), _ptr(act_mask), ws.data_ptr() if nws else None, nws,
