@@ -24,7 +24,7 @@ DB = int(os.environ.get("SITEBENCH_DECODER_B", "16"))  # decoder sites: both wit
 def site_list(ops):
     out = []
     for op in ops:
-        if op == "corr_fwd":
+        if op in ("corr_fwd", "corr_fwd_leaky"):
             out += [(op, (DB, C, H, W)) for C, H, W in KITTI]
         elif op in ("corr_bwd", "corr_bwd_leaky"):
             out += [(op, (DB, C, H, W, True, True)) for C, H, W in KITTI]
@@ -60,6 +60,8 @@ def alg_bytes(op, key):
     B, C, H, W = key[:4]
     if op == "corr_fwd":
         return 4 * B * H * W * (2 * C + 81)
+    if op == "corr_fwd_leaky":  # + the sign mask written
+        return 4 * B * H * W * (2 * C + 81) + 8 * _lib.load().usf_corr_act_mask_words(B, H, W, 4)
     if op == "corr_bwd":
         return 4 * B * H * W * (81 + 4 * C)
     if op == "corr_bwd_leaky":  # + the derivative's input: the sign mask, else the activated output

@@ -447,46 +447,61 @@ __global__ __launch_bounds__(64 * NDY * CS) void corr_fwd_kernel(const float* __
   float* ob = out + (size_t)b * ep.out_bstride + (size_t)dy * K * HW + y * W + xb;
   const bool leaky = ep.act != 0;
   const float slope = ep.slope;
-  auto epi = [&](float a) {
-    const float v = a / cf;
-    return leaky ? (v > 0.f ? v : v * slope) : v;
+  // The channel mean v = acc / C as the reference rounds it. For a power-of-two C
+  // (KITTI L1, L3, L4) the product with 1/C is the same number (exact scaling, one
+  // rounding) without the IEEE division sequence. The branch is uniform; each
+  // path is the whole epilogue (stores, then the sign mask).
+  auto epilogue = [&](auto mean, auto pos) {
+    auto epi = [&](float a) {
+      const float v = mean(a);
+      return leaky ? (v > 0.f ? v : v * slope) : v;
+    };
+    const bool vec = ((W & 3) == 0) && ((ep.out_bstride & 3) == 0) && (xb + PX <= W);
+#pragma unroll
+    for (int dx = 0; dx < K; ++dx) {
+      float* o = ob + dx * HW;
+      if (vec) {
+#pragma unroll
+        for (int i = 0; i < PX / 4; ++i)
+          reinterpret_cast<float4*>(o)[i] = make_float4(epi(acc[dx][4 * i]), epi(acc[dx][4 * i + 1]),
+                                                        epi(acc[dx][4 * i + 2]), epi(acc[dx][4 * i + 3]));
+      } else {
+#pragma unroll
+        for (int i = 0; i < PX; ++i)
+          if (xb + i < W) o[i] = epi(acc[dx][i]);
+      }
+    }
+    if (leaky && ep.mask && xb < W) {
+      // sign bits of this lane's activated outputs, one word per 4-pixel quad
+      // (the epilogue's test v = mean(acc) > 0, as pos()); bits past W stay 0
+      unsigned long long* mw = ep.mask + ((size_t)(b * K + dy) * H + y) * ((W + 3) >> 2) + (xb >> 2);
+      // one bit per dx nibble, replicated: masks the columns past W of a partial quad
+      constexpr unsigned long long kRep = [] {
+        unsigned long long r = 0;
+        for (int dx = 0; dx < K; ++dx) r |= 1ull << (4 * dx);
+        return r;
+      }();
+#pragma unroll
+      for (int j = 0; j < PX / 4; ++j) {
+        unsigned long long bits = 0;
+#pragma unroll
+        for (int dx = 0; dx < K; ++dx)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            bits |= (unsigned long long)pos(acc[dx][4 * j + i]) << (4 * dx + i);
+        const int nv = W - (xb + 4 * j);  // valid columns of this quad (> 0 for quads in the row)
+        if (nv > 0) mw[j] = nv >= 4 ? bits : bits & (kRep * ((1ull << nv) - 1));
+      }
+    }
   };
-  const bool vec = ((W & 3) == 0) && ((ep.out_bstride & 3) == 0) && (xb + PX <= W);
-#pragma unroll
-  for (int dx = 0; dx < K; ++dx) {
-    float* o = ob + dx * HW;
-    if (vec) {
-#pragma unroll
-      for (int i = 0; i < PX / 4; ++i)
-        reinterpret_cast<float4*>(o)[i] = make_float4(epi(acc[dx][4 * i]), epi(acc[dx][4 * i + 1]),
-                                                      epi(acc[dx][4 * i + 2]), epi(acc[dx][4 * i + 3]));
-    } else {
-#pragma unroll
-      for (int i = 0; i < PX; ++i)
-        if (xb + i < W) o[i] = epi(acc[dx][i]);
-    }
-  }
-  if (leaky && ep.mask && xb < W) {
-    // sign bits of this lane's activated outputs, one word per 4-pixel quad
-    // (the same test as the epilogue's: v = acc / C > 0); bits past W stay 0
-    unsigned long long* mw = ep.mask + ((size_t)(b * K + dy) * H + y) * ((W + 3) >> 2) + (xb >> 2);
-    // one bit per dx nibble, replicated: masks the columns past W of a partial quad
-    constexpr unsigned long long kRep = [] {
-      unsigned long long r = 0;
-      for (int dx = 0; dx < K; ++dx) r |= 1ull << (4 * dx);
-      return r;
-    }();
-#pragma unroll
-    for (int j = 0; j < PX / 4; ++j) {
-      unsigned long long bits = 0;
-#pragma unroll
-      for (int dx = 0; dx < K; ++dx)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          bits |= (unsigned long long)(acc[dx][4 * j + i] / cf > 0.f) << (4 * dx + i);
-      const int nv = W - (xb + 4 * j);  // valid columns of this quad (> 0 for quads in the row)
-      if (nv > 0) mw[j] = nv >= 4 ? bits : bits & (kRep * ((1ull << nv) - 1));
-    }
+  if ((C & (C - 1)) == 0) {
+    // C = 2^k: v = RN(a 2^-k) > 0 exactly when a > 2^(k-150) (below that the
+    // product rounds to zero), so the sign test needs no second product
+    const float inv = 1.0f / cf;
+    const float thr = C > 1 ? (cf * 0x1p-75f) * 0x1p-75f : 0.f;  // 2^(k-150), exact for k >= 1
+    epilogue([&](float a) { return a * inv; }, [&](float a) { return a > thr; });
+  } else {
+    epilogue([&](float a) { return a / cf; }, [&](float a) { return a / cf > 0.f; });
   }
 }
 
