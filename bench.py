@@ -100,7 +100,7 @@ def kernel_report(summary, device, steps, replay=True):
     """Per call site: in-step time (events around each launch in the timed
     region), device time of graph-replayed launches, algorithmic GB/s and HBM
     fraction; plus the roofline of the dominant site (by in-step time)."""
-    from unsamflow_amd.kernel_timer import device_time_us, site_launcher, site_name
+    from unsamflow_amd.kernel_timer import device_time_cold_us, device_time_us, site_launcher, site_name
 
     rows, per_op = [], {}
     best = best_dev = None
@@ -110,18 +110,25 @@ def kernel_report(summary, device, steps, replay=True):
         row = {
             "op": op, "shape": list(key), "site": site_name(op, key), "calls_per_step": calls,
             "in_step_us": round(us, 2), "bytes": a["bytes"],
-            "gbps_in_step": round(a["bytes"] / (us * 1e-6) / 1e9, 1),
             "hbm_frac_in_step": round(a["bytes"] / (us * 1e-6) / 1e9 / HBM_PEAK_GBPS, 4),
         }
         if replay:
-            # the per-level HBM fraction uses the DEVICE time: at small sites the
-            # in-step interval also holds the GPU catching up with the host
-            # (2-4x rocprof at L0-L2, profiles/r01_v22_roofline_check.json)
-            dev_us = device_time_us(site_launcher(op, key, device, seed=i))
+            # the per-level HBM fraction uses the COLD device time (read-flushed
+            # caches before every launch: inputs come from HBM, as in the step for
+            # the large levels); the warm graph replay keeps L3/L4 working sets in
+            # the 256 MB Infinity Cache and overstates HBM. At small
+            # sites the in-step interval also holds the GPU catching up with the
+            # host (2-4x rocprof at L0-L2, profiles/r01_v22_roofline_check.json).
+            fn = site_launcher(op, key, device, seed=i)
+            dev_us = device_time_us(fn)
+            cold_us = device_time_cold_us(fn)
+            del fn
             row["device_us"] = round(dev_us, 2)
-            row["gbps"] = round(a["bytes"] / (dev_us * 1e-6) / 1e9, 1)
-            row["hbm_frac"] = round(a["bytes"] / (dev_us * 1e-6) / 1e9 / HBM_PEAK_GBPS, 4)
-            row["tflops"] = round(a["flops"] / (dev_us * 1e-6) / 1e12, 2)
+            row["cold_us"] = round(cold_us, 2)
+            row["gbps"] = round(a["bytes"] / (cold_us * 1e-6) / 1e9, 1)
+            row["hbm_frac"] = round(a["bytes"] / (cold_us * 1e-6) / 1e9 / HBM_PEAK_GBPS, 4)
+            row["hbm_frac_warm"] = round(a["bytes"] / (dev_us * 1e-6) / 1e9 / HBM_PEAK_GBPS, 4)
+            row["tflops"] = round(a["flops"] / (cold_us * 1e-6) / 1e12, 2)
             if best_dev is None or calls * dev_us > best_dev[0]:
                 best_dev = (calls * dev_us, row)
         rows.append(row)
@@ -134,7 +141,7 @@ def kernel_report(summary, device, steps, replay=True):
         "kernel": row["op"],
         "shape": row["shape"],
         "site": row["site"],
-        "achieved": row["gbps_in_step"],
+        "achieved": round(row["bytes"] / (row["in_step_us"] * 1e-6) / 1e9, 1),
         "peak": HBM_PEAK_GBPS,
         "unit": "GB/s",
         "frac": row["hbm_frac_in_step"],
@@ -142,6 +149,7 @@ def kernel_report(summary, device, steps, replay=True):
         "mean_us": row["in_step_us"],
         "launches_timed": int(round(row["calls_per_step"] * steps)),
         "replay_us": row.get("device_us"),
+        "cold_us": row.get("cold_us"),
         "traffic": None,
         "method": "algorithmic bytes (SURVEY 8d) / mean duration of the site's launches in the timed region "
                   "(HIP events on the launch stream)",
@@ -153,7 +161,7 @@ def kernel_report(summary, device, steps, replay=True):
         # flows): the model's own random-init flows are near zero, which
         # flatters the warp backward's scatter in-step
         d = best_dev[1]
-        roof["dominant_by_device"] = {"site": d["site"], "device_us": d["device_us"], "gbps": d["gbps"],
+        roof["dominant_by_device"] = {"site": d["site"], "device_us": d["device_us"], "cold_us": d["cold_us"],
                                       "frac": d["hbm_frac"], "us_per_step": round(best_dev[0], 1)}
     return rows, roof, {k: round(v, 1) for k, v in per_op.items()}
 
@@ -181,14 +189,24 @@ SURVEY_CONFIGS = {"cfg1": (2, 32, 64, 128), "cfg2": (8, 128, 32, 104)}  # SURVEY
 
 
 def copy_ceiling_gbps(device, mib=512, reps=10):
-    """Measured device-to-device copy rate (read + write bytes / time)."""
-    a = torch.empty(mib * 1024 * 1024 // 4, device=device)
+    """Measured device-to-device copy rate (read + write bytes / time) of the
+    library's float4 STREAM copy (usf_stream_copy_f32; MI355X_MICROARCH.md
+    measures 6.29 TB/s this way, torch's copy_ reached only 4.7-5.3)."""
+    from unsamflow_amd import _lib
+
+    lib = _lib.load()
+    a = torch.ones(mib * 1024 * 1024 // 4, device=device)
     b = torch.empty_like(a)
-    b.copy_(a)
+    stream = _lib.stream_handle(device)
+
+    def copy():
+        _lib.check(lib.usf_stream_copy_f32(a.data_ptr(), b.data_ptr(), a.numel(), stream), "usf_stream_copy_f32")
+
+    copy()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(reps):
-        b.copy_(a)
+        copy()
     e1.record()
     e1.synchronize()
     sec = e0.elapsed_time(e1) / 1e3 / reps
@@ -215,11 +233,19 @@ def pmc_traffic(op, shape):
 def survey_configs_gpu(device):
     from unsamflow_amd.kernel_timer import device_time_us, site_launcher
 
+    from unsamflow_amd.kernel_timer import corr_bytes, device_time_cold_us
+
     out = {}
     for name, (B, C, H, W) in SURVEY_CONFIGS.items():
-        f = device_time_us(site_launcher("corr_fwd", (B, C, H, W), device))
-        b = device_time_us(site_launcher("corr_bwd", (B, C, H, W, True, True), device))
-        out[name] = {"shape": [B, C, H, W], "fwd_us": round(f, 2), "bwd_us": round(b, 2)}
+        ff = site_launcher("corr_fwd", (B, C, H, W), device)
+        fb = site_launcher("corr_bwd", (B, C, H, W, True, True), device)
+        f, b = device_time_us(ff), device_time_us(fb)
+        fc, bc = device_time_cold_us(ff), device_time_cold_us(fb)
+        nf, nb = corr_bytes(B, C, H, W), corr_bytes(B, C, H, W, backward=True)
+        out[name] = {"shape": [B, C, H, W], "fwd_us": round(f, 2), "bwd_us": round(b, 2),
+                     "fwd_cold_us": round(fc, 2), "bwd_cold_us": round(bc, 2),
+                     "fwd_hbm_frac": round(nf / (f * 1e-6) / 1e9 / HBM_PEAK_GBPS, 3),
+                     "bwd_hbm_frac": round(nb / (b * 1e-6) / 1e9 / HBM_PEAK_GBPS, 3)}
     return out
 
 
@@ -487,12 +513,18 @@ def main():
                 "max_displacement": 4,
                 "parallelism": f"dp{world}",
             },
-            "roofline": roof,
-            "cpu_baseline": cpu,
+            "final_loss": round(loss_val, 6),
+            # per call site, compact (the driver keeps the last 8 KB of stdout, so the
+            # summaries below come after this list): algorithmic bytes per launch,
+            # in-step mean, warm graph-replay and cold (read-flushed) device times;
+            # hbm_frac uses the cold time, hbm_frac_warm the replay
+            "levels": None if rows is None else [
+                {k: r[k] for k in ("site", "calls_per_step", "bytes", "in_step_us", "device_us", "cold_us",
+                                   "hbm_frac", "hbm_frac_warm") if k in r} for r in rows],
             "hot_path_us_per_step": per_op_us,
             "survey_configs": gpu_configs,
-            "levels": rows,
-            "final_loss": round(loss_val, 6),
+            "cpu_baseline": cpu,
+            "roofline": roof,
         }
         if not on_gpu:
             out["device"] = "cpu (launcher test: oracle ops, not a measurement)"

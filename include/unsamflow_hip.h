@@ -65,8 +65,12 @@
 extern "C" {
 #endif
 
-#define USF_ABI_VERSION 5
+#define USF_ABI_VERSION 6
 #define USF_EINVAL (-1)
+#define USF_EDEVICE (-2) /* a kernel raised a device error flag (USF_SYNC_CHECK=1 only) */
+
+/* device error flags (usf_device_errors) */
+#define USF_DEVERR_WARP_OVERFLOW 1 /* binned warp backward: overflow list past its capacity */
 
 /* padding modes for the warp (flow_warp `pad` argument) */
 #define USF_PAD_ZEROS 0
@@ -288,14 +292,25 @@ int usf_convex_upsample_bwd_f32(const float* flow, const float* mask, const floa
 int usf_area_pyramid_f32(const float* x, float* out1, float* out2, float* out3, int B, int C,
                          int H, int W, void* stream);
 
+/* Device-side error flags raised by kernels since the last clear (a bitmask
+ * of USF_DEVERR_*; 0 = none), after synchronising `stream`; clear != 0 resets
+ * them. -1 if the synchronisation or the read failed. With USF_SYNC_CHECK=1
+ * every entry point checks them after its launch and returns USF_EDEVICE. */
+int usf_device_errors(void* stream, int clear);
+
+/* STREAM copy of n floats (16-byte lanes; src and dst 16-byte aligned, n % 4
+ * == 0): a measurement helper, bench.py's device-copy ceiling. */
+int usf_stream_copy_f32(const float* src, float* dst, long long n, void* stream);
+
 /* Tuning hook (benchmarking only; not needed for correct use).
  * Forces kernel variant `index` of `op` for d=4 launches in this process:
  * op 0 = correlation forward tile config, op 1 = correlation backward tile
  * config, op 2 = warp grad_x scatter (0 = wave reduce-by-key + direct global
  * atomics, 1 = LDS-aggregated tiles, 2 / 3 = variant 0 with 4 / 1 channel
  * slices per workgroup, 4 = gather for |flow| < 2 px + scatter for the rest,
- * 5 = scatter over vertically adjacent pixel pairs);
- * index -1 restores the built-in choice. Returns the number of
+ * 5 = scatter over vertically adjacent pixel pairs), op 3 = photometric
+ * loss kernel (0 = row-streaming strips, the default; 1 = the workgroup-tile
+ * kernel it replaced, kept for A/B timing); index -1 restores the built-in choice. Returns the number of
  * variants of `op` (so index range is [0, n)), or USF_EINVAL for an unknown op
  * or out-of-range index. Process-wide; set it before launching, not
  * concurrently with launches. */

@@ -23,9 +23,11 @@ def _run(args, env_extra=None, timeout=600):
 
 
 @pytest.mark.timeout(900)
-def test_bench_spawns_two_ranks_on_gloo():
+@pytest.mark.parametrize("config", ["kitti", "sintel_mf"])
+def test_bench_spawns_two_ranks_on_gloo(config):
+    hw = ["64", "128"] if config == "kitti" else ["128", "256"]  # sintel_mf: its capture size (test_ddp_cpu)
     p = _run(["--device", "cpu", "--gpus", "2", "--steps", "1", "--warmup", "0", "--batch", "1",
-              "--hw", "64", "128"])
+              "--hw", *hw, "--config", config])
     assert p.returncode == 0, p.stderr[-3000:]
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, p.stdout  # rank 0 only
@@ -35,6 +37,8 @@ def test_bench_spawns_two_ranks_on_gloo():
     assert out["config"]["global_batch"] == 2 and out["config"]["per_gpu_batch"] == 1
     assert out["scaling"] == "weak"
     assert out["value"] > 0 and out["device"].startswith("cpu")
+    assert ("Sintel" in out["metric"]) == (config == "sintel_mf")
+    assert out["final_loss"] == out["final_loss"]  # finite (not NaN)
 
 
 @pytest.mark.timeout(300)

@@ -40,7 +40,7 @@ def test_header_declares_the_abi():
          "usf_photo_loss_bwd_f32",
          "usf_flow_upsample_f32", "usf_flow_upsample_bwd_f32", "usf_area_pyramid_f32",
          "usf_convex_upsample_f32", "usf_convex_upsample_bwd_scratch", "usf_convex_upsample_bwd_f32",
-         "usf_set_variant"]
+         "usf_set_variant", "usf_device_errors", "usf_stream_copy_f32"]
     )
 
 
@@ -59,7 +59,7 @@ def test_library_exports_every_declared_symbol(lib):
 def test_abi_version(lib):
     from unsamflow_amd import _lib
 
-    assert lib.usf_abi_version() == _lib.ABI_VERSION == 5
+    assert lib.usf_abi_version() == _lib.ABI_VERSION == 6
 
 
 def test_no_torch_types_in_abi():
@@ -133,7 +133,8 @@ def test_variant_override_bounds(lib):
     n_bwd = lib.usf_set_variant(1, -1)
     assert n_fwd > 1 and n_bwd > 1
     assert lib.usf_set_variant(0, n_fwd) == -1 and b"bad op" in lib.usf_last_error_string()
-    assert lib.usf_set_variant(3, 0) == -1
+    assert lib.usf_set_variant(4, 0) == -1
+    assert lib.usf_set_variant(3, 1) == 2 and lib.usf_set_variant(3, -1) == 2  # photometric: strip / tile
     assert lib.usf_set_variant(2, 1) == 7 and lib.usf_set_variant(2, -1) == 7
     assert lib.usf_set_variant(1, n_bwd - 1) == n_bwd
     assert lib.usf_set_variant(1, -1) == n_bwd

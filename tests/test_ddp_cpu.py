@@ -21,40 +21,47 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, out_dir):
+def _worker(rank, world, port, out_dir, cfg_name="kitti"):
     sys.path.insert(0, REPO)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.set_num_threads(2)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from oracle.hashrng import hash_init_
     from oracle.torch_ref import OracleCorrelation, oracle_flow_warp, oracle_occu_mask_backward
-    from unsamflow_amd.config import kitti_base
+    from unsamflow_amd.config import kitti_base, sintel_mf
     from unsamflow_amd.harness import TrainStep, synthetic_pair
 
-    cfg = kitti_base()
+    # sintel_mf: SURVEY config 5, the mask-feature branch (SAM segments one-hot
+    # encoded, pwclite.py:355-357) under DDP, as the reference's Sintel run
+    # (train.py:116-120, 228-234)
+    cfg = kitti_base() if cfg_name == "kitti" else sintel_mf()
     step = TrainStep(cfg, "cpu", ddp=True, corr_module=OracleCorrelation(4), warp_fn=oracle_flow_warp,
                      occ_backward_fn=oracle_occu_mask_backward)
     hash_init_(step.module, seed=3)
     # DDP broadcast happened at construction; re-sync after the deterministic init
     for p in step.module.parameters():
         dist.broadcast(p.data, 0)
-    img1, img2, _, _ = synthetic_pair(1, 64, 128, "cpu", seed=100 + rank)
+    # sintel_mf at its golden-capture size (tests/golden/pwclite_sintel_mf.npz): at 64x128
+    # this config's backward has non-finite feature-pyramid gradients even on one
+    # process (its coarsest levels shrink to a few pixels), so replicas cannot be compared
+    hw = (64, 128) if cfg_name == "kitti" else (128, 256)
+    img1, img2, s1, s2 = synthetic_pair(1, *hw, "cpu", seed=100 + rank, with_seg=cfg_name != "kitti")
 
     # local gradient without communication
     with step.model.no_sync():  # forward AND backward inside: no all-reduce
-        loss_local, _ = step.forward_loss(img1, img2)
+        loss_local, _ = step.forward_loss(img1, img2, s1, s2)
         loss_local.backward()
     local = [p.grad.detach().clone() for p in step.module.parameters()]
     step.optimizer.zero_grad(set_to_none=True)
 
     # DDP gradient (all-reduce average)
-    loss, _ = step.forward_loss(img1, img2)
+    loss, _ = step.forward_loss(img1, img2, s1, s2)
     loss.backward()
     ddp = [p.grad.detach().clone() for p in step.module.parameters()]
     torch.save({"local": local, "ddp": ddp}, os.path.join(out_dir, f"rank{rank}.pt"))
 
     # a full optimizer step keeps the replicas in sync
-    step(img1, img2)
+    step(img1, img2, s1, s2)
     flat = torch.cat([p.detach().reshape(-1) for p in step.module.parameters()])
     gathered = [torch.zeros_like(flat) for _ in range(world)]
     dist.all_gather(gathered, flat)
@@ -63,9 +70,10 @@ def _worker(rank, world, port, out_dir):
 
 
 @pytest.mark.timeout(600)
-def test_ddp_two_ranks_gloo(tmp_path):
+@pytest.mark.parametrize("cfg_name", ["kitti", "sintel_mf"])
+def test_ddp_two_ranks_gloo(tmp_path, cfg_name):
     world = 2
-    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), cfg_name), nprocs=world, join=True)
     r0 = torch.load(tmp_path / "rank0.pt", weights_only=True)
     r1 = torch.load(tmp_path / "rank1.pt", weights_only=True)
     for a, b, l0, l1 in zip(r0["ddp"], r1["ddp"], r0["local"], r1["local"]):

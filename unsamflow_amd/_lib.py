@@ -17,7 +17,7 @@ from pathlib import Path
 import torch  # noqa: F401  (load torch's HIP runtime before the plugin)
 
 _LIB_PATH = Path(os.environ.get("USF_LIB", Path(__file__).resolve().parent / "lib" / "libunsamflow_hip.so"))
-ABI_VERSION = 5
+ABI_VERSION = 6
 PAD_ZEROS = 0
 PAD_BORDER = 1
 
@@ -105,6 +105,8 @@ _SIGNATURES = {
     ),
     "usf_area_pyramid_f32": ([_c_float_p] * 4 + [ctypes.c_int] * 4 + [ctypes.c_void_p], ctypes.c_int),
     "usf_set_variant": ([ctypes.c_int, ctypes.c_int], ctypes.c_int),
+    "usf_device_errors": ([ctypes.c_void_p, ctypes.c_int], ctypes.c_int),
+    "usf_stream_copy_f32": ([_c_float_p, _c_float_p, ctypes.c_longlong, ctypes.c_void_p], ctypes.c_int),
 }
 EXPORTED_SYMBOLS = tuple(_SIGNATURES)
 

@@ -23,15 +23,16 @@ INCLUDE_DIR = PKG_DIR.parent / "include"
 ARCH = os.environ.get("USF_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
-SOURCES = ["corr.hip", "warp.hip", "photo.hip", "upsample.hip", "convex.hip", "capi.cpp"]
+SOURCES = ["corr.hip", "warp.hip", "photo.hip", "upsample.hip", "convex.hip", "stream.hip", "capi.cpp"]
 HEADERS = ["usf_common.h", "warp_tap.h"]
 
 # -fno-slp-vectorize: the SLP vectorizer packs the kernels' independent FMAs into
 # v_pk_fma_f32 / v_pk_add_f32, whose operands must sit in aligned register pairs:
 # it then re-reads the correlation windows at odd LDS offsets (ds_read2_b32) and
-# adds v_mov shuffles, and serialises each window's reads with its FMAs. Plain
-# v_fma_f32 issues the same FLOPs at the same rate (64 FLOP/clk/SIMD either way,
-# MI355X_MICROARCH.md) without that. Measured on the box (profiles/ab_r01/slp_*.json):
+# adds v_mov shuffles, and serialises each window's reads with its FMAs. The
+# packing gains little FLOP rate on gfx950: plain v_fmac_f32 measured 102-107 TF,
+# v_pk_fma_f32 106-122 TF (4-13 % more; profiles/r02_fma_rate.json), far less than
+# those costs. Measured on the box (profiles/ab_r01/slp_*.json):
 # corr bwd L4 54.8 -> 41.1 us, L3 40.3 -> 30.5 us; corr fwd L3 17.6 -> 15.7 us;
 # photometric pair 91.5 -> 84.9 us; warp unchanged.
 COMMON_FLAGS = [

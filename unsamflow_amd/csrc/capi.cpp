@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <climits>
+#include <cstdint>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -66,6 +67,12 @@ static int finish(const char* fn, hipError_t e, hipStream_t s) {
   if (e == hipSuccess && sync_check()) {
     e = hipStreamSynchronize(s);
     if (e != hipSuccess) fprintf(stderr, "[usf] %s: fault after launch: %s\n", fn, hipGetErrorString(e));
+    const int flags = e == hipSuccess ? device_errors(s, true) : 0;
+    if (flags > 0) {
+      fprintf(stderr, "[usf] %s: device error flags 0x%x\n", fn, flags);
+      set_error("%s: device error flags 0x%x", fn, flags);
+      return USF_EDEVICE;
+    }
   }
   if (e != hipSuccess) {
     set_error("%s: HIP launch failed: %s (%d)", fn, hipGetErrorString(e), (int)e);
@@ -536,9 +543,27 @@ int usf_area_pyramid_f32(const float* x, float* out1, float* out2, float* out3, 
                 (hipStream_t)stream);
 }
 
+int usf_stream_copy_f32(const float* src, float* dst, long long n, void* stream) {
+  clear_error();
+  if (!src || !dst || n <= 0 || n % 4 != 0 || (reinterpret_cast<uintptr_t>(src) & 15) ||
+      (reinterpret_cast<uintptr_t>(dst) & 15)) {
+    set_error("usf_stream_copy_f32: need 16-byte aligned pointers and n %% 4 == 0 (n=%lld)", n);
+    return USF_EINVAL;
+  }
+  if (const int pe = pre_check("usf_stream_copy_f32", (hipStream_t)stream)) return pe;
+  return finish("usf_stream_copy_f32", stream_copy_launch(src, dst, n, (hipStream_t)stream), (hipStream_t)stream);
+}
+
+int usf_device_errors(void* stream, int clear) {
+  clear_error();
+  const int v = device_errors((hipStream_t)stream, clear != 0);
+  if (v < 0) set_error("usf_device_errors: stream sync or flag read failed");
+  return v;
+}
+
 int usf_set_variant(int op, int index) {
   clear_error();
-  if (op < 0 || op > 2 || index < -1 || index >= variant_count(op)) {
+  if (op < 0 || op > 3 || index < -1 || index >= variant_count(op)) {
     set_error("usf_set_variant: bad op %d / index %d", op, index);
     return USF_EINVAL;
   }

@@ -863,7 +863,8 @@ __device__ __forceinline__ void bwd_stage(const float (&gv)[DYW][K][PX], const f
 // partial slot), and write channels [c0, c0 + CC) of the tile, divided by C.
 template <int D, int PX, int SEGX, int NW, int CC, int V>
 __device__ __forceinline__ void bwd_combine(const float* red, float* gxb, int t1, int nthr, int c0,
-                                            int cend, int y0, int x0, int H, int W, float cf) {
+                                            int cend, int y0, int x0, int H, int W, float cf, float fc,
+                                            bool pow2) {
   using F = BwdCfg<D, PX, SEGX, NW, CC, V>;
   constexpr int TW = F::TW, TH = F::TH;
   const int HW = H * W;
@@ -884,14 +885,15 @@ __device__ __forceinline__ void bwd_combine(const float* red, float* gxb, int t1
     const int yy = y0 + py, xx = x0 + pxo;
     if (c0 + c < cend && yy < H) {
       float* o4 = gxb + (size_t)(c0 + c) * HW + yy * W + xx;
-#if USF_BWD_RCP
-      // the channel mean as a multiply by 1/C (exact for power-of-two C, else
-      // within 1 ulp of the division): an IEEE division is ~10 VALU
-      // instructions, 4 per quad (profiles/ab_r02)
-      sum.x *= cf; sum.y *= cf; sum.z *= cf; sum.w *= cf;
-#else
-      sum.x /= cf; sum.y /= cf; sum.z /= cf; sum.w /= cf;
-#endif
+      // the channel mean: for power-of-two C a multiply by 1/C, which is the
+      // same number as the division (scaling by 2^-k rounds once); for other C
+      // the IEEE division the reference does (correlation_cuda_kernel.cu:204,
+      // 297; ~10 VALU instructions per element, only at those levels)
+      if (USF_BWD_RCP && pow2) {
+        sum.x *= cf; sum.y *= cf; sum.z *= cf; sum.w *= cf;
+      } else {
+        sum.x /= fc; sum.y /= fc; sum.z /= fc; sum.w /= fc;
+      }
       if (vec_out && xx + 3 < W) {
         *reinterpret_cast<float4*>(o4) = sum;
       } else {
@@ -967,7 +969,8 @@ __device__ __forceinline__ void corr_bwd_tile(float* sm, const float* __restrict
   const rsrc_t rx = plane_rsrc(xsb, true, C * HW * 4);
   auto dma_stage = [&](int c0, float* img) { sx.load(rx, img, wave, c0, cend, HW); };
 
-  const float cf = USF_BWD_RCP ? 1.f / (float)C : (float)C;  // bwd_combine's scale
+  const float cf = 1.f / (float)C, fc = (float)C;  // bwd_combine's scale (exact: power-of-two C only)
+  const bool pow2 = (C & (C - 1)) == 0;
   float* gxb = gx + (size_t)b * C * HW;
   dma_stage(cbeg, sm);
   dma_wait_all();
@@ -986,7 +989,7 @@ __device__ __forceinline__ void corr_bwd_tile(float* sm, const float* __restrict
 #if defined(USF_BWD_PROBE) && USF_BWD_PROBE == 3
     continue;  // probe: no combine, no second barrier (timing only)
 #endif
-    bwd_combine<D, PX, SEGX, NW, CC, V>(red, gxb, tid, NT, c0, cend, y0, x0, H, W, cf);
+    bwd_combine<D, PX, SEGX, NW, CC, V>(red, gxb, tid, NT, c0, cend, y0, x0, H, W, cf, fc, pow2);
     __syncthreads();  // partial slices free for the next stage
     USF_TRACE_AT(6 + 4 * st);
   }
@@ -1183,9 +1186,9 @@ hipError_t leaky_bwd_gather_launch(const float* g, const float* act, long long g
 namespace {
 }  // namespace
 
-static int g_variant[3] = {-1, -1, -1};
+static int g_variant[4] = {-1, -1, -1, -1};
 int variant_override(int op) { return __atomic_load_n(&g_variant[op], __ATOMIC_RELAXED); }
-int variant_count(int op) { return op == 0 ? kFwdCandidates : op == 1 ? kBwdCandidates : 7; }
+int variant_count(int op) { return op == 0 ? kFwdCandidates : op == 1 ? kBwdCandidates : op == 2 ? 7 : 2; }
 void set_variant_override(int op, int index) { __atomic_store_n(&g_variant[op], index, __ATOMIC_RELAXED); }
 
 hipError_t corr_fwd_launch(const float* x1, const float* x2, float* out, int B, int C, int H,

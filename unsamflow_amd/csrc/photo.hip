@@ -43,7 +43,9 @@
 // pixels. Window statistics use FMAs and a hardware reciprocal (the loss is
 // checked against the reference at a stated tolerance); the warp coordinate
 // chain keeps the reference rounding (warp_tap.h).
+#include <algorithm>
 #include <cstdint>
+#include <cstdlib>
 
 #include "usf_common.h"
 #include "warp_tap.h"
@@ -459,8 +461,473 @@ __global__ __launch_bounds__(256) void photo_bwd_kernel(const float* __restrict_
   }
 }
 
+// ------------------------------------------------------- strip (row-stream) --
+// photo_strip_kernel: the same per-direction result as photo_fwd_kernel,
+// organised for gfx950's wave instead of a workgroup tile. One WAVE owns a
+// strip of 64 staged columns (lanes; the 60 middle ones are its own pixels)
+// by R own rows and streams down it, one staged row per step:
+//   stage row r   -> lane l holds x = rec*m, y = tgt*m of column x0-2+l (C channels)
+//   row sums      -> 3-column sums of x, y, x^2, y^2, xy by two DPP adds each
+//                    (v_add_f32_dpp wave_shl:1: lane l reads lane l+1)
+//   window r-2    -> the three latest row sums (kept in registers) give the 3x3
+//                    window whose top-left row is r-2: SSIM, and with GRAD the
+//                    coefficients alpha, beta, gamma of its pixel derivative
+//   pixel row r-2 -> the 3x3 box sums of alpha/beta/gamma around each pixel
+//                    (vertical in registers, horizontal by DPP wave_shr:1)
+//                    complete its gradient basis.
+// No LDS, no barriers: the waves of a workgroup are independent (4 per
+// workgroup only to fill CUs in fewer dispatches). Each staged pixel is
+// warped once; the halo is 2 rows above and below each strip (R chosen per
+// shape, strip_rows) and 2 columns either side. The next row's flow, mask and
+// target loads are issued one step ahead. Work items are (sample, strip,
+// direction) with the direction fastest, so both directions of a strip run
+// side by side on one CU and share the two frames' lines in L1/L2.
+#ifndef USF_PHOTO_WAVES
+#define USF_PHOTO_WAVES 2  // waves per SIMD the strip kernel's registers are sized for
+#endif
+constexpr int kSL = 64;        // lanes of a strip = staged columns
+constexpr int kSO = kSL - 4;   // own columns per strip (lanes 2 .. 61)
+constexpr int kOffNone = 0x7FFFFFF0;  // buffer offset past num_records: reads 0
+constexpr int kRsrcWord3 = 0x00020000;
+
+struct StripArgs {
+  PhotoDir dir[2];
+  long long fbs, bbs;
+  int B, H, W, R, nsx, nsy, ndir, nitems;
+};
+
+// lane l reads lane l+1 / l-1 of the wave (DPP wave_shl:1 / wave_shr:1;
+// the missing neighbour of lane 63 / 0 reads 0). Every lane must be active.
+// mov_dpp with bound_ctrl (no "old" operand to materialise), so the compiler
+// folds it into the add that consumes it (v_add_f32_dpp).
+__device__ __forceinline__ float from_next(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x130, 0xf, 0xf, true));
+}
+__device__ __forceinline__ float from_prev(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x138, 0xf, 0xf, true));
+}
+__device__ __forceinline__ float hsum_next(float v) { return v + from_next(v + from_next(v)); }  // v[l]+v[l+1]+v[l+2]
+__device__ __forceinline__ float hsum_prev(float v) { return v + from_prev(v + from_prev(v)); }  // v[l]+v[l-1]+v[l-2]
+
+struct Sums {   // window statistics need only x, y, x^2 + y^2 and xy
+  float x, y, q, xy;
+};
+
+// SSIM of one window from its sums over the 9 pixels, and with GRAD the
+// coefficients of dS/dx_p = alpha + beta x_p + gamma y_p (see ssim_window)
+template <bool GRAD>
+__device__ __forceinline__ float ssim_sums(const Sums& s, float& al, float& be, float& ga) {
+  constexpr float k9 = 1.0f / 9.0f;
+  const float mx = s.x * k9, my = s.y * k9;
+  const float exy = s.xy * k9;
+  const float mxy = mx * my;
+  const float m2 = fmaf(mx, mx, my * my);                  // mx^2 + my^2
+  const float A1 = fmaf(2.f, mxy, kC1), A2 = fmaf(2.f, exy - mxy, kC2);
+  const float B1 = m2 + kC1;
+  const float B2 = fmaf(s.q, k9, -m2) + kC2;              // sig_x + sig_y + C2
+  const float rd = __builtin_amdgcn_rcpf(B1 * B2);
+  const float r = (A1 * A2) * rd;
+  const float raw = fmaf(-0.5f, r, 0.5f);
+  const float cl = __builtin_amdgcn_fmed3f(raw, 0.f, 1.f);
+  if constexpr (GRAD) {
+    const bool pass = cl == raw;  // torch.clamp passes the gradient for 0 <= raw <= 1
+    const float k = pass ? -k9 * rd : 0.f;
+    al = k * fmaf(-r * mx, B2 - B1, my * (A2 - A1));
+    be = (k * -r) * B1;
+    ga = k * A1;
+  }
+  return cl;
+}
+
+// The warp tap of warp_tap.h (same rounding, same results) with the border
+// clip as selects instead of branches, and the four corner byte offsets for
+// buffer loads: a masked corner gets an offset past num_records, which the
+// hardware reads as 0 (no value selects after the loads).
+struct TapB {
+  int onw, one, osw, ose;
+  float n, s, w, e, mx, my;
+};
+template <bool BORDER>
+__device__ __forceinline__ TapB make_tap_b(float u, float v, int x, int y, int H, int W) {
+#pragma clang fp contract(off)
+  TapB t;
+  const float wm1 = (float)(W - 1), hm1 = (float)(H - 1);
+  const float gx = 2.0f * ((float)x + u) / wm1 - 1.0f;
+  const float gy = 2.0f * ((float)y + v) / hm1 - 1.0f;
+  const float sx = wm1 / 2.0f, sy = hm1 / 2.0f;
+  float ix = (gx + 1.0f) * sx;
+  float iy = (gy + 1.0f) * sy;
+  t.mx = sx;
+  t.my = sy;
+  if (BORDER) {
+    const bool xlo = !(ix > 0.f), xhi = ix >= wm1, ylo = !(iy > 0.f), yhi = iy >= hm1;
+    ix = xlo ? 0.f : (xhi ? wm1 : ix);
+    iy = ylo ? 0.f : (yhi ? hm1 : iy);
+    t.mx = (xlo || xhi) ? 0.f : sx;
+    t.my = (ylo || yhi) ? 0.f : sy;
+  }
+  const float fx = floorf(ix), fy = floorf(iy);
+  t.w = ix - fx;
+  t.e = 1.0f - t.w;
+  t.n = iy - fy;
+  t.s = 1.0f - t.n;
+  const int xw = (int)fx, yn = (int)fy;
+  const bool vxw = (unsigned)xw < (unsigned)W, vxe = (unsigned)(xw + 1) < (unsigned)W;
+  const bool vyn = (unsigned)yn < (unsigned)H, vys = (unsigned)(yn + 1) < (unsigned)H;
+  const int o = 4 * (yn * W + xw);
+  t.onw = vxw && vyn ? o : kOffNone;
+  t.one = vxe && vyn ? o + 4 : kOffNone;
+  t.osw = vxw && vys ? o + 4 * W : kOffNone;
+  t.ose = vxe && vys ? o + 4 * W + 4 : kOffNone;
+  return t;
+}
+
+// One wave's strip, as a stream of staged rows. Every ring (loads of rows r
+// and r+1, row sums of rows r-2..r, window coefficients of window rows
+// q-2..q, pixel state of rows r-2..r) has period 3, and step<PH> handles the
+// rows with r = y0 - 2 + i, i = PH mod 3, so all ring slots are compile-time
+// registers: no copies between steps.
+template <bool BORDER, bool GRAD, int C>
+struct Strip {
+  // per-wave constants: buffer resources of the sample's source planes (gathers),
+  // flow, mask, target (row loads) and basis (stores); 32-bit byte offsets
+  __amdgpu_buffer_rsrc_t rs[C], rflow, rmask, rtgt, rbas;
+  int H, W, HW, y0, rown, col, cc, lane;
+  bool col_in, lane_own, wcol;
+  float fxs, fys;
+  // rings (period 3). The memory work of a row runs ahead of its arithmetic:
+  // its flow is loaded two steps early, its tap evaluated and its gathers,
+  // target and mask loads issued one step early, so a wave's gather latency
+  // overlaps the previous row's window and basis work.
+  float fu[3], fv[3];                        // flow of a row
+  float gv[3][C][4], tt[3][C], mm[3];        // gathered corners (nw, ne, sw, se), target, mask
+  float tn[3], tw[3], tmx[3], tmy[3];        // tap distances (s = 1 - n, e = 1 - w) and coordinate factors
+  Sums sm[3][C];                             // row sums of x, y, x^2 + y^2, xy
+  float ca[3][C], cb[3][C], cg[3][C];        // window coefficients alpha, beta, gamma
+  // pixel state from its staging to the completion of its basis two steps later
+  // ({dix*kx, diy*ky, x, y} per channel, 12 floats packed in 3 float4s): in LDS,
+  // this wave's own planes [slot][chunk][lane] (16-byte lanes, conflict-free),
+  // which keeps the kernel at 3 waves per SIMD
+  float4* pend;
+  float l1, ssum, msum;
+
+  // Every memory instruction of a step is issued on every path: rows outside
+  // the image or past the strip, and lanes that own no output, use a byte
+  // offset past num_records (loads read 0, stores are dropped) instead of a
+  // branch. The compiler's s_waitcnt then counts the same instructions on all
+  // paths and can wait for row r's gathers without waiting for row r+1's (a
+  // branch around a load made it wait for everything, vmcnt(0)).
+  __device__ __forceinline__ static float ld(__amdgpu_buffer_rsrc_t r, int off, int soff) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, soff, 0));
+  }
+  __device__ __forceinline__ void st(float v, int off, int soff) {
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(int, v), rbas, off, soff, 0);
+  }
+  __device__ __forceinline__ int row_off(int r, bool ok) const {
+    return ok && r >= 0 && r < H ? 4 * (r * W + cc) : kOffNone;
+  }
+  template <int slot>
+  __device__ __forceinline__ void load_flow(int r, bool ok) {
+    const int o = row_off(r, ok);
+    fu[slot] = ld(rflow, o, 0);
+    fv[slot] = ld(rflow, o, 4 * HW);
+  }
+  // the row's tap, then its gathers and its target / mask loads (not waited for)
+  template <int slot>
+  __device__ __forceinline__ void issue(int r, bool ok) {
+    const TapB tp = make_tap_b<BORDER>(fu[slot], fv[slot], cc, r, H, W);
+    const int o = row_off(r, ok);
+    const bool in = o != kOffNone;
+    const int onw = in ? tp.onw : kOffNone, one = in ? tp.one : kOffNone;
+    const int osw = in ? tp.osw : kOffNone, ose = in ? tp.ose : kOffNone;
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      gv[slot][c][0] = ld(rs[c], onw, 0);
+      gv[slot][c][1] = ld(rs[c], one, 0);
+      gv[slot][c][2] = ld(rs[c], osw, 0);
+      gv[slot][c][3] = ld(rs[c], ose, 0);
+      tt[slot][c] = ld(rtgt, o, 4 * c * HW);
+    }
+    mm[slot] = ld(rmask, o, 0);
+    tn[slot] = tp.n;
+    tw[slot] = tp.w;
+    tmx[slot] = tp.mx;
+    tmy[slot] = tp.my;
+  }
+
+  template <int PH>
+  __device__ __forceinline__ void step(int i, int nsteps) {
+    constexpr int S0 = PH, S1 = (PH + 2) % 3, S2 = (PH + 1) % 3;  // slots of rows r, r-1, r-2
+    const int r = y0 - 2 + i;
+    // rows r+2 and r+1 reuse the memory-side slots of rows r-1 and r-2
+    load_flow<S1>(r + 2, i + 2 < nsteps);
+    issue<S2>(r + 1, i + 1 < nsteps);
+
+    // ---- stage row r: x = rec * m, y = tgt * m (all loads read 0 outside the image)
+    const bool own_row = i >= 2 && i < rown + 2;  // wave-uniform
+    float x[C], y[C];
+    const float n = tn[S0], w = tw[S0];
+    float s, e;
+    {
+#pragma clang fp contract(off)
+      s = 1.0f - n;  // as make_tap_b computes them
+      e = 1.0f - w;
+    }
+    const float (&v)[C][4] = gv[S0];
+    const float m = mm[S0];
+    const float me = col_in ? m : 0.f;
+    float rec[C];
+    {
+#pragma clang fp contract(off)
+      const float wnw = s * e, wne = s * w, wsw = n * e, wse = n * w;
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        rec[c] = v[c][0] * wnw + v[c][1] * wne + v[c][2] * wsw + v[c][3] * wse;
+        x[c] = rec[c] * me;
+        y[c] = tt[S0][c] * me;
+      }
+    }
+    float ax = 0.f, ay = 0.f, kx = 0.f, ky = 0.f;
+    float pk[4 * C];
+#pragma unroll
+    for (int k = 0; k < 4 * C; ++k) pk[k] = 0.f;
+    if (own_row) {  // compute only
+      const float mo = lane_own ? m : 0.f;  // L1 / mask sums: own pixels only
+      kx = m * tmx[S0] * fxs;
+      ky = m * tmy[S0] * fys;
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        const float diff = rec[c] - tt[S0][c];
+        l1 += fabsf(diff) * mo;
+        if constexpr (GRAD) {
+          const float dix = (v[c][1] - v[c][0]) * s + (v[c][3] - v[c][2]) * n;
+          const float diy = (v[c][2] - v[c][0]) * e + (v[c][3] - v[c][1]) * w;
+          const float sg = diff > 0.f ? 1.f : (diff < 0.f ? -1.f : 0.f);
+          ax += sg * dix;
+          ay += sg * diy;
+          pk[4 * c] = dix * kx;
+          pk[4 * c + 1] = diy * ky;
+          pk[4 * c + 2] = x[c];
+          pk[4 * c + 3] = y[c];
+        }
+      }
+      msum += mo;
+    }
+    if constexpr (GRAD) {
+#pragma unroll
+      for (int k = 0; k < C; ++k)
+        pend[(S0 * C + k) * 64 + lane] = make_float4(pk[4 * k], pk[4 * k + 1], pk[4 * k + 2], pk[4 * k + 3]);
+      const int o = own_row && lane_own ? 4 * (r * W + col) : kOffNone;
+      st(ax * kx, o, 0);
+      st(ay * ky, o, 4 * HW);
+    }
+
+    // ---- row sums of row r
+#pragma unroll
+    for (int c = 0; c < C; ++c)
+      sm[S0][c] = Sums{hsum_next(x[c]), hsum_next(y[c]), hsum_next(fmaf(x[c], x[c], y[c] * y[c])),
+                       hsum_next(x[c] * y[c])};
+
+    // ---- window with top-left row q = r - 2, then pixel row q's gradient basis
+    const int q = r - 2;
+    const bool qown = i >= 4;  // q is an own row of this strip (wave-uniform)
+    float4 pq[C];              // pixel row q's state
+    if constexpr (GRAD) {
+#pragma unroll
+      for (int k = 0; k < C; ++k) pq[k] = pend[(S2 * C + k) * 64 + lane];
+    }
+    float bx = 0.f, by = 0.f;
+    if (i >= 2) {  // compute only
+      const bool wrow = q >= 0 && q <= H - 3;  // wave-uniform
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        float al = 0.f, be = 0.f, ga = 0.f;
+        if (wrow) {
+          const Sums& a2 = sm[S2][c];
+          const Sums& a1 = sm[S1][c];
+          const Sums& a0 = sm[S0][c];
+          const Sums w{a2.x + a1.x + a0.x, a2.y + a1.y + a0.y, a2.q + a1.q + a0.q, a2.xy + a1.xy + a0.xy};
+          const float s = ssim_sums<GRAD>(w, al, be, ga);
+          if (qown && lane_own && wcol) ssum += s;
+          if (!wcol) al = be = ga = 0.f;
+        }
+        if constexpr (GRAD) {
+          ca[S0][c] = al;
+          cb[S0][c] = be;
+          cg[S0][c] = ga;
+          if (qown) {
+            const float ha = hsum_prev(ca[S2][c] + ca[S1][c] + al);
+            const float hb = hsum_prev(cb[S2][c] + cb[S1][c] + be);
+            const float hg = hsum_prev(cg[S2][c] + cg[S1][c] + ga);
+            const float ds = fmaf(hg, pq[c].w, fmaf(hb, pq[c].z, ha));  // sum over windows q' of p
+            bx = fmaf(ds, pq[c].x, bx);
+            by = fmaf(ds, pq[c].y, by);
+          }
+        }
+      }
+    }
+    if constexpr (GRAD) {
+      const int o = qown && lane_own ? 4 * (q * W + col) : kOffNone;
+      st(bx, o, 8 * HW);
+      st(by, o, 12 * HW);
+    }
+  }
+};
+
+template <bool BORDER, bool GRAD, int C>
+__global__ __launch_bounds__(256, USF_PHOTO_WAVES) void photo_strip_kernel(StripArgs a, float* __restrict__ partials) {
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(xcd_remap(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6));
+  if (wid >= a.nitems) return;
+  int rest = wid;
+  int dirn = 0;
+  if (a.ndir == 2) {
+    dirn = rest & 1;
+    rest >>= 1;
+  }
+  const int sx = rest % a.nsx;
+  rest /= a.nsx;
+  const int sy = rest % a.nsy;
+  const int b = rest / a.nsy;
+  const PhotoDir dr = a.dir[dirn];
+  __shared__ float4 pend_lds[GRAD ? 4 * 3 * C * 64 : 1];
+  Strip<BORDER, GRAD, C> st;
+  st.pend = pend_lds + (threadIdx.x >> 6) * (3 * C * 64);
+  st.H = a.H;
+  st.W = a.W;
+  st.HW = a.H * a.W;
+  const int x0 = sx * kSO;
+  st.y0 = sy * a.R;
+  st.rown = min(a.R, a.H - st.y0);
+  st.lane = lane;
+  st.col = x0 - 2 + lane;
+  st.cc = min(max(st.col, 0), a.W - 1);
+  st.col_in = st.col >= 0 && st.col < a.W;
+  st.lane_own = lane >= 2 && lane < 2 + kSO && st.col < a.W;
+  st.wcol = st.col >= 0 && st.col <= a.W - 3;  // window with top-left column col is valid
+  const size_t HW = (size_t)st.HW;
+  const float* srcb = dr.src + (size_t)b * C * HW;
+  const int pb = st.HW * 4;  // plane bytes (< 2^31, capi.cpp)
+#pragma unroll
+  for (int c = 0; c < C; ++c)
+    st.rs[c] = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(srcb + (size_t)c * HW), 0, pb, kRsrcWord3);
+  st.rtgt = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(dr.tgt + (size_t)b * C * HW), 0, C * pb, kRsrcWord3);
+  st.rmask = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(dr.mask + (size_t)b * HW), 0, pb, kRsrcWord3);
+  st.rflow = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(dr.flow + b * a.fbs), 0, 2 * pb, kRsrcWord3);
+  if constexpr (GRAD)
+    st.rbas = __builtin_amdgcn_make_buffer_rsrc(dr.basis + b * a.bbs, 0, 4 * pb, kRsrcWord3);
+  st.fxs = 2.0f / (float)(a.W - 1);
+  st.fys = 2.0f / (float)(a.H - 1);
+#pragma unroll
+  for (int k = 0; k < 3; ++k)
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      st.sm[k][c] = Sums{0.f, 0.f, 0.f, 0.f};
+      st.ca[k][c] = st.cb[k][c] = st.cg[k][c] = 0.f;
+    }
+  st.l1 = st.ssum = st.msum = 0.f;
+  const int nsteps = st.rown + 4;
+  st.template load_flow<0>(st.y0 - 2, true);
+  st.template load_flow<1>(st.y0 - 1, true);
+  st.template issue<0>(st.y0 - 2, true);
+  int i = 0;
+  for (; i + 3 <= nsteps; i += 3) {
+    st.template step<0>(i, nsteps);
+    st.template step<1>(i + 1, nsteps);
+    st.template step<2>(i + 2, nsteps);
+  }
+  if (i < nsteps) st.template step<0>(i, nsteps);
+  if (i + 1 < nsteps) st.template step<1>(i + 1, nsteps);
+
+  // ---- wave partials (fixed-order butterflies), one slot per (direction, sample, strip)
+  float l1 = st.l1, ssum = st.ssum, msum = st.msum;
+#pragma unroll
+  for (int s = 32; s > 0; s >>= 1) {
+    l1 += __shfl_xor(l1, s);
+    ssum += __shfl_xor(ssum, s);
+    msum += __shfl_xor(msum, s);
+  }
+  if (lane == 0) {
+    float* o = partials + 3 * (((size_t)dirn * a.B + b) * a.nsy * a.nsx + (size_t)sy * a.nsx + sx);
+    o[0] = l1;
+    o[1] = ssum;
+    o[2] = msum;
+  }
+}
+
+// Own rows per strip: every wave of a launch does the same (R + 4)-step
+// stream, so the launch takes about max(waves per SIMD, 2) x (R + 4) steps
+// (below 2 waves per SIMD a lone wave issues at half rate, so fewer waves no
+// longer help). The smallest such product wins; ties go to the smaller R.
+constexpr int kStripRows[] = {4, 6, 8, 12, 16, 20, 24, 32};
+constexpr int kSimds = 1024;  // 256 CUs x 4 SIMDs
+
+int strip_rows(int B, int H, int W, int ndir) {
+  static const int forced = [] {  // USF_PHOTO_ROWS=R: tuning override (tools/photoab.py)
+    const char* v = getenv("USF_PHOTO_ROWS");
+    return v ? atoi(v) : 0;
+  }();
+  if (forced >= kStripRows[0]) return forced;  // (partials are sized for R >= 4)
+  const long long nsx = (W + kSO - 1) / kSO;
+  int best = kStripRows[0];
+  long long best_cost = -1;
+  for (int R : kStripRows) {
+    const long long waves = (long long)ndir * B * nsx * ((H + R - 1) / R);
+    const long long per_simd = std::max<long long>((waves + kSimds - 1) / kSimds, 2);
+    const long long cost = per_simd * (std::min(R, H) + 4);
+    if (best_cost < 0 || cost < best_cost) {
+      best_cost = cost;
+      best = R;
+    }
+  }
+  return best;
+}
+
+template <bool BORDER, bool GRAD>
+hipError_t strip_launch_c(const StripArgs& sa, int C, dim3 grid, float* partials, hipStream_t s) {
+  if (C == 3)
+    hipLaunchKernelGGL((photo_strip_kernel<BORDER, GRAD, 3>), grid, dim3(256), 0, s, sa, partials);
+  else if (C == 2)
+    hipLaunchKernelGGL((photo_strip_kernel<BORDER, GRAD, 2>), grid, dim3(256), 0, s, sa, partials);
+  else
+    hipLaunchKernelGGL((photo_strip_kernel<BORDER, GRAD, 1>), grid, dim3(256), 0, s, sa, partials);
+  return hipGetLastError();
+}
+
+hipError_t photo_strip_launch(const PhotoArgs& a, int ndir, int pad_mode, float* partials, float* out,
+                              float w_l1, float w_ssim, hipStream_t s) {
+  StripArgs sa{};
+  sa.dir[0] = a.dir[0];
+  sa.dir[1] = a.dir[1];
+  sa.fbs = a.fbs;
+  sa.bbs = a.bbs;
+  sa.B = a.B;
+  sa.H = a.H;
+  sa.W = a.W;
+  sa.R = strip_rows(a.B, a.H, a.W, ndir);
+  sa.nsx = (a.W + kSO - 1) / kSO;
+  sa.nsy = (a.H + sa.R - 1) / sa.R;
+  sa.ndir = ndir;
+  sa.nitems = ndir * a.B * sa.nsx * sa.nsy;
+  const dim3 grid((unsigned)((sa.nitems + 3) / 4));
+  const bool grad = a.dir[0].basis != nullptr;
+  hipError_t e;
+  if (pad_mode == 1)
+    e = grad ? strip_launch_c<true, true>(sa, a.C, grid, partials, s) : strip_launch_c<true, false>(sa, a.C, grid, partials, s);
+  else
+    e = grad ? strip_launch_c<false, true>(sa, a.C, grid, partials, s) : strip_launch_c<false, false>(sa, a.C, grid, partials, s);
+  if (e != hipSuccess) return e;
+  const double n1 = (double)a.B * a.C * a.H * a.W;
+  const double n2 = (a.H >= 3 && a.W >= 3) ? (double)a.B * a.C * (a.H - 2) * (a.W - 2) : 0.0;
+  const double n3 = (double)a.B * a.H * a.W;
+  hipLaunchKernelGGL(photo_final_kernel, dim3((unsigned)ndir), dim3(kFinNT), 0, s, partials,
+                     a.B * sa.nsx * sa.nsy, out, n1, n2, n3, w_l1, w_ssim);
+  return hipGetLastError();
+}
+
 hipError_t photo_launch(const PhotoArgs& a, int ndir, int pad_mode, float* partials, float* out,
                         float w_l1, float w_ssim, hipStream_t s) {
+  if (variant_override(3) != 1) return photo_strip_launch(a, ndir, pad_mode, partials, out, w_l1, w_ssim, s);
   const int tiles_y = (a.H + kTH - 1) / kTH;
   const int ntiles = a.tiles_x * tiles_y;
   const dim3 grid((unsigned)ntiles, (unsigned)a.B, (unsigned)ndir);
@@ -489,7 +956,10 @@ hipError_t photo_launch(const PhotoArgs& a, int ndir, int pad_mode, float* parti
 }  // namespace
 
 int photo_partials(int B, int H, int W) {
-  return 3 * B * ((H + kTH - 1) / kTH) * ((W + kTW - 1) / kTW);
+  // either kernel, any strip height (the smallest R has the most strips)
+  const int tile = 3 * B * ((H + kTH - 1) / kTH) * ((W + kTW - 1) / kTW);
+  const int strip = 3 * B * ((H + kStripRows[0] - 1) / kStripRows[0]) * ((W + kSO - 1) / kSO);
+  return std::max(tile, strip);
 }
 
 hipError_t photo_fwd_launch(const float* src, const float* tgt, const float* mask, const float* flow,

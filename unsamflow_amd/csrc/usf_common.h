@@ -4,7 +4,13 @@
 #include <cstddef>
 #include <cstdint>
 
+#include "unsamflow_hip.h"
+
 namespace usf {
+
+// Device-side error flags (warp.hip): read and optionally cleared after a
+// stream sync; -1 if the sync or the copy failed.
+int device_errors(hipStream_t s, bool clear);
 
 // Thread-local error slot behind usf_last_error_string().
 void set_error(const char* fmt, ...);
@@ -128,6 +134,7 @@ hipError_t convex_fwd_launch(const float* flow, const float* mask, float* out, i
 hipError_t convex_bwd_launch(const float* flow, const float* mask, const float* gout, float* gflow,
                              float* gmask, float* scratch, int B, int H, int W, int factor,
                              float mask_scale, hipStream_t s);
+hipError_t stream_copy_launch(const float* src, float* dst, long long n, hipStream_t s);
 hipError_t area_pyramid_launch(const float* x, float* o1, float* o2, float* o3, long long planes,
                                int H, int W, hipStream_t s);
 

@@ -583,13 +583,24 @@ __global__ __launch_bounds__(256) void warp_gx_bins_kernel(const float* __restri
 // corner) the large-shift field took 111 us at L4 on same-address atomics.
 // The loop bound is the device-side list length: nothing overflowed, nothing runs.
 constexpr int kOvfCh = 4;
+
+// Device-side error flags of this code object (usf_device_errors() reads and
+// clears them; USF_SYNC_CHECK=1 reports them after every launch). A list
+// length past its capacity can only come from stale per-call state (the
+// capacity is one entry per pixel); the pass then stops at the capacity and
+// raises USF_DEVERR_WARP_OVERFLOW instead of silently dropping entries.
+__device__ int g_dev_errors = 0;
+
 template <bool BORDER>
 __global__ __launch_bounds__(256) void warp_gx_ovf_kernel(const float* __restrict__ flow, long long fbs,
                                                           const float* __restrict__ gout, BinArgs ba,
                                                           float* __restrict__ gx, int C, int H, int W) {
   const int HW = H * W;
-  const int n = min(*ba.novf, ba.ovf_cap);
+  const int listed = *ba.novf;
+  const int n = min(listed, ba.ovf_cap);
   const int lane = threadIdx.x & 63;
+  if ((listed < 0 || listed > ba.ovf_cap) && blockIdx.x == 0 && threadIdx.x == 0)
+    atomicOr(&g_dev_errors, USF_DEVERR_WARP_OVERFLOW);
   const int ngrp = (C + kOvfCh - 1) / kOvfCh;
   const long long units = (long long)((n + 63) / 64) * ngrp;  // (64-entry chunk, channel group)
   const long long nw = (long long)gridDim.x * (blockDim.x >> 6);
@@ -1318,6 +1329,17 @@ __global__ __launch_bounds__(256) void occ_threshold_kernel(float* __restrict__ 
 }
 
 }  // namespace
+
+int device_errors(hipStream_t s, bool clear) {
+  int v = 0;
+  if (hipStreamSynchronize(s) != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_dev_errors), sizeof(int)) != hipSuccess) return -1;
+  if (clear && v != 0) {
+    const int z = 0;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_dev_errors), &z, sizeof(int)) != hipSuccess) return -1;
+  }
+  return v;
+}
 
 hipError_t warp_fwd_launch(const float* x, const float* flow, long long fbs, float* out, int B,
                            int C, int H, int W, int pad_mode, hipStream_t s) {

@@ -232,6 +232,40 @@ def site_launcher(op: str, key, device, seed: int = 0):
     return lambda: ops.warp_backward(x, flow, go, pad, need_x, need_flow)
 
 
+_flush = {}
+
+
+def device_time_cold_us(fn, reps: int = 8, flush_mib: int = 512) -> float:
+    """Mean duration of one ``fn()`` launch from cold caches (HBM-honest).
+
+    Before every timed launch a read sweep over a ``flush_mib`` MiB scratch
+    buffer (a sum into one element: reads only, so no dirty lines are written
+    back during the timed launch; a write flush overshot) evicts
+    the 256 MiB Infinity Cache and the L2s. Two events bracket the launch alone
+    on the launch stream; the sweep runs for ~0.1 ms, long enough for the host
+    to enqueue the launch before the GPU reaches it, so the interval holds no
+    host gap. The outputs of the previous launch are written back during the
+    sweep, not during the timed launch."""
+    dev = torch.cuda.current_device()
+    if dev not in _flush:
+        _flush[dev] = (torch.ones(flush_mib * 1024 * 1024 // 4, device="cuda"), torch.empty((), device="cuda"))
+    buf, sink = _flush[dev]
+    for _ in range(2):
+        fn()
+    evs = []
+    for _ in range(reps):
+        torch.sum(buf, dim=0, out=sink)
+        s = torch.cuda.Event(enable_timing=True)
+        e = torch.cuda.Event(enable_timing=True)
+        s.record()
+        fn()
+        e.record()
+        evs.append((s, e))
+    torch.cuda.synchronize()
+    times = sorted(s.elapsed_time(e) * 1e3 for s, e in evs)
+    return sum(times[1:-1]) / (len(times) - 2) if len(times) > 2 else times[0]
+
+
 def device_time_us(fn, reps: int = 20, iters: int = 5) -> float:
     """Mean device time of one ``fn()`` launch: REPS launches in a HIP graph, replayed."""
     side = torch.cuda.Stream()

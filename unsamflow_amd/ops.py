@@ -175,7 +175,15 @@ def warp_backward(
     need_x: bool = True,
     need_flow: bool = True,
 ) -> tuple[torch.Tensor | None, torch.Tensor | None]:
-    """(grad_x, grad_flow) of :func:`warp_forward`. grad_x uses fp32 atomics."""
+    """(grad_x, grad_flow) of :func:`warp_forward`.
+
+    grad_x is the library's binned gather (``usf_warp_bwd_ex_f32``): every
+    source pixel is filed under its north-west corner cell and each target cell
+    sums its sources in a fixed order, so grad_x is deterministic unless a cell
+    receives more than 4 source pixels (strongly compressive flow), whose
+    excess is added with fp32 atomics. The call allocates a workspace of
+    ``usf_warp_bwd_workspace(B, H, W)`` bytes (about 88 B per pixel) from
+    torch's caching allocator. grad_flow is deterministic."""
     _require_device_f32("x", x)
     _require_device_f32("flow12", flow)
     _require_device_f32("grad_output", grad_out)
@@ -326,7 +334,9 @@ def photo_loss_pair_forward(flow, im1, im2, mask1, mask2, pad: str = "border", w
     partials = torch.empty(2 * lib.usf_photo_loss_partials(B, H, W), device=im1.device, dtype=torch.float32)
     out = torch.empty(6, device=im1.device, dtype=torch.float32)
     basis = torch.empty((B, 8, H, W), device=im1.device, dtype=torch.float32) if need_grad else None
-    nbytes = 2 * 4 * B * H * W * (2 * C + 3 + (4 if need_grad else 0))
+    # algorithmic bytes (each input read once): im1 and im2 (2C), the
+    # 4-channel flow, both masks; with the gradient the 8 basis planes written once
+    nbytes = 4 * B * H * W * (2 * C + 4 + 2 + (8 if need_grad else 0))
     op = "photo_pair_grad" if need_grad else "photo_pair"
     with torch.cuda.device(im1.device), _kt.timed(op, (B, C, H, W, pad), im1.device, nbytes):
         rc = lib.usf_photo_loss_pair_fwd_f32(a.data_ptr(), b_.data_ptr(), m1.data_ptr(), m2.data_ptr(),
