@@ -186,6 +186,10 @@ def atomic_floor(shape, mean_us):
 
 
 SURVEY_CONFIGS = {"cfg1": (2, 32, 64, 128), "cfg2": (8, 128, 32, 104)}
+# a `levels` row: call site, launches per step, algorithmic bytes per launch, in-step
+# mean us, warm graph-replay us, cold (read-flushed) us, HBM fraction from the cold
+# time (the HBM-honest one), HBM fraction from the warm replay
+LEVEL_FIELDS = ["site", "calls_per_step", "bytes", "in_step_us", "device_us", "cold_us", "hbm_frac", "hbm_frac_warm"]
 
 
 def copy_ceiling_gbps(device, mib=512, reps=10):
@@ -363,23 +367,36 @@ def launch_ranks(n: int) -> int:
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]], env=env))
     rc = 0
     live = list(procs)
-    while live:
-        for p in list(live):
-            code = p.poll()
-            if code is None:
-                continue
-            live.remove(p)
-            if code != 0 and rc == 0:
-                rc = code
-                for q in live:
-                    q.terminate()
-        time.sleep(0.2)
+    try:
+        while live:
+            for p in list(live):
+                code = p.poll()
+                if code is None:
+                    continue
+                live.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code
+                    for q in live:
+                        q.terminate()
+            time.sleep(0.2)
+    finally:  # the parent interrupted or failing: no orphaned rank keeps its GPU or the port
+        for q in live:
+            q.terminate()
+        for q in live:
+            try:
+                q.wait(timeout=10)
+            except subprocess.TimeoutExpired:
+                q.kill()
     return rc
 
 
 def main():
     args = parse()
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        import signal
+
+        # SIGTERM to the launcher ends its ranks too (launch_ranks' finally)
+        signal.signal(signal.SIGTERM, lambda *_: sys.exit(143))
         sys.exit(launch_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -514,13 +531,10 @@ def main():
                 "parallelism": f"dp{world}",
             },
             "final_loss": round(loss_val, 6),
-            # per call site, compact (the driver keeps the last 8 KB of stdout, so the
-            # summaries below come after this list): algorithmic bytes per launch,
-            # in-step mean, warm graph-replay and cold (read-flushed) device times;
-            # hbm_frac uses the cold time, hbm_frac_warm the replay
-            "levels": None if rows is None else [
-                {k: r[k] for k in ("site", "calls_per_step", "bytes", "in_step_us", "device_us", "cold_us",
-                                   "hbm_frac", "hbm_frac_warm") if k in r} for r in rows],
+            # per call site, one compact row each (the driver keeps the last 8 KB of
+            # stdout, so the summaries below come after this list)
+            "levels_fields": LEVEL_FIELDS,
+            "levels": None if rows is None else [[r.get(k) for k in LEVEL_FIELDS] for r in rows],
             "hot_path_us_per_step": per_op_us,
             "survey_configs": gpu_configs,
             "cpu_baseline": cpu,

@@ -165,8 +165,8 @@ int usf_warp_bwd_f32(const float* x, const float* flow, long long flow_bstride,
                      int B, int C, int H, int W, int pad_mode, void* stream);
 
 /* usf_warp_bwd_f32 with a caller workspace of usf_warp_bwd_workspace(B,H,W)
- * bytes (device memory, no alignment beyond 256 B needed; contents need not
- * be initialised and are scratch after return). With it, gx is computed by
+ * bytes (device memory, 16-byte aligned -- USF_EINVAL otherwise; contents need
+ * not be initialised and are scratch after return). With it, gx is computed by
  * a binned gather: every source pixel is filed under the cell of its
  * north-west corner, then each target cell sums weight * gout over the
  * pixels filed under it and its three up-left neighbours in a fixed order,

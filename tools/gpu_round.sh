@@ -4,7 +4,7 @@
 set -o pipefail
 R=$(pwd)
 mkdir -p gpurun_out
-timeout -k 10 600 python -m pytest tests -q -m gpu -x > gpurun_out/pytest_gpu.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -q -m gpu -x --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
 rc=$?; echo "pytest rc=$rc" >> gpurun_out/pytest_gpu.log; tail -4 gpurun_out/pytest_gpu.log
 [ $rc -eq 0 ] || { grep -E "^E |Error" gpurun_out/pytest_gpu.log | head -20; exit 1; }
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { echo "smoke failed rc=$?"; tail gpurun_out/smoke.log; exit 1; }

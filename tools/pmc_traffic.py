@@ -109,13 +109,20 @@ def main():
         elif op == "photo_fwd_grad":
             alg = 4 * B * H * W * (2 * C + 7)  # + the [B,4,H,W] gradient basis written
         elif op == "photo_pair_grad":
-            alg = 2 * 4 * B * H * W * (2 * C + 7)  # both directions
+            # both directions, every input read once: im1, im2, flow4,
+            # both masks; the 8 basis planes written once (ops.photo_loss_pair_forward)
+            alg = 4 * B * H * W * (2 * C + 4 + 2 + 8)
         else:
             alg = 4 * B * H * W * 6 * ndir  # photo_bwd: basis in, grad_flow out
         traffic = fk * 1024 * f_read + wk * 1024 * f_write
-        sites.append({"op": op, "shape": list(key), "fetch_kib": round(fk, 1), "write_kib": round(wk, 1),
-                      "traffic_bytes": int(traffic), "algorithmic_bytes": int(alg),
-                      "traffic_over_algorithmic": round(traffic / alg, 3)})
+        row = {"op": op, "shape": list(key), "fetch_kib": round(fk, 1), "write_kib": round(wk, 1),
+               "read_bytes": int(fk * 1024 * f_read), "write_bytes": int(wk * 1024 * f_write),
+               "traffic_bytes": int(traffic), "algorithmic_bytes": int(alg),
+               "traffic_over_algorithmic": round(traffic / alg, 3)}
+        if op == "photo_pair_grad":  # reads against the read-once minimum (48 B/px at C = 3)
+            row["read_once_bytes"] = 4 * B * H * W * (2 * C + 4 + 2)
+            row["read_over_read_once"] = round(row["read_bytes"] / row["read_once_bytes"], 3)
+        sites.append(row)
     print(json.dumps({"calibration": {"copy_bytes": COPY_BYTES, "fetch_scale": round(f_read, 4),
                                       "write_scale": round(f_write, 4), "launches_per_site": n},
                       "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes, --kernel-trace only) "

@@ -23,7 +23,10 @@ def main():
     roof = bench["roofline"]
     steps = bench["steps"] + bench["warmup"]
     sites = []
-    for row in bench["levels"]:
+    levels = bench["levels"]
+    if levels and isinstance(levels[0], list):  # compact rows (bench.py LEVEL_FIELDS)
+        levels = [dict(zip(bench["levels_fields"], r)) for r in levels]
+    for row in levels:
         st = stats.get(row["site"])
         entry = {"site": row["site"], "bench_in_step_us": row["in_step_us"], "rocprof_avg_us": None,
                  "rocprof_calls": int(st["Calls"]) if st else None}

@@ -272,6 +272,10 @@ static int warp_bwd_common(const char* fn, const float* x, const float* flow, lo
     set_error("%s: negative workspace size", fn);
     return USF_EINVAL;
   }
+  if (ws && (reinterpret_cast<uintptr_t>(ws) & 15)) {  // the binned gather reads it with 16-byte loads
+    set_error("%s: workspace must be 16-byte aligned", fn);
+    return USF_EINVAL;
+  }
   if (const int pe = pre_check(fn, (hipStream_t)stream)) return pe;
   return finish(fn,
                 warp_bwd_launch(x, flow, flow_bstride, gout, gx, gflow, B, C, H, W, pad_mode,

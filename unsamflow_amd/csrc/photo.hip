@@ -478,7 +478,7 @@ __global__ __launch_bounds__(256) void photo_bwd_kernel(const float* __restrict_
 // No LDS, no barriers: the waves of a workgroup are independent (4 per
 // workgroup only to fill CUs in fewer dispatches). Each staged pixel is
 // warped once; the halo is 2 rows above and below each strip (R chosen per
-// shape, strip_rows) and 2 columns either side. The next row's flow, mask and
+// shape, strip_plan) and 2 columns either side. The next row's flow, mask and
 // target loads are issued one step ahead. Work items are (sample, strip,
 // direction) with the direction fastest, so both directions of a strip run
 // side by side on one CU and share the two frames' lines in L1/L2.
@@ -655,7 +655,12 @@ struct Strip {
     tmy[slot] = tp.my;
   }
 
-  template <int PH>
+  // ST / WIN / BAS: whether row r is an own row (staged with its gradient
+  // state), window row r - 2 is computed, pixel row r - 2's basis completes:
+  // 0 = never, 1 = always, 2 = decided at run time. The strip's interior steps
+  // run with all three known true (no branches, no value merges); the first
+  // four and the last two to four steps decide at run time.
+  template <int PH, int ST = 2, int WIN = 2, int BAS = 2>
   __device__ __forceinline__ void step(int i, int nsteps) {
     constexpr int S0 = PH, S1 = (PH + 2) % 3, S2 = (PH + 1) % 3;  // slots of rows r, r-1, r-2
     const int r = y0 - 2 + i;
@@ -664,7 +669,7 @@ struct Strip {
     issue<S2>(r + 1, i + 1 < nsteps);
 
     // ---- stage row r: x = rec * m, y = tgt * m (all loads read 0 outside the image)
-    const bool own_row = i >= 2 && i < rown + 2;  // wave-uniform
+    const bool own_row = ST == 2 ? (i >= 2 && i < rown + 2) : ST == 1;  // wave-uniform
     float x[C], y[C];
     const float n = tn[S0], w = tw[S0];
     float s, e;
@@ -730,15 +735,16 @@ struct Strip {
 
     // ---- window with top-left row q = r - 2, then pixel row q's gradient basis
     const int q = r - 2;
-    const bool qown = i >= 4;  // q is an own row of this strip (wave-uniform)
+    const bool qown = BAS == 2 ? i >= 4 : BAS == 1;  // q is an own row of this strip (wave-uniform)
     float4 pq[C];              // pixel row q's state
     if constexpr (GRAD) {
 #pragma unroll
       for (int k = 0; k < C; ++k) pq[k] = pend[(S2 * C + k) * 64 + lane];
     }
     float bx = 0.f, by = 0.f;
-    if (i >= 2) {  // compute only
-      const bool wrow = q >= 0 && q <= H - 3;  // wave-uniform
+    if (WIN == 2 ? i >= 2 : WIN == 1) {  // compute only
+      // (in interior steps q is an own row, so 0 <= q <= H - 3 holds)
+      const bool wrow = WIN == 1 || (q >= 0 && q <= H - 3);  // wave-uniform
 #pragma unroll
       for (int c = 0; c < C; ++c) {
         float al = 0.f, be = 0.f, ga = 0.f;
@@ -748,7 +754,7 @@ struct Strip {
           const Sums& a0 = sm[S0][c];
           const Sums w{a2.x + a1.x + a0.x, a2.y + a1.y + a0.y, a2.q + a1.q + a0.q, a2.xy + a1.xy + a0.xy};
           const float s = ssim_sums<GRAD>(w, al, be, ga);
-          if (qown && lane_own && wcol) ssum += s;
+          ssum += qown && lane_own && wcol ? s : 0.f;
           if (!wcol) al = be = ga = 0.f;
         }
         if constexpr (GRAD) {
@@ -797,8 +803,9 @@ __global__ __launch_bounds__(256, USF_PHOTO_WAVES) void photo_strip_kernel(Strip
   st.W = a.W;
   st.HW = a.H * a.W;
   const int x0 = sx * kSO;
-  st.y0 = sy * a.R;
-  st.rown = min(a.R, a.H - st.y0);
+  // balanced strips: heights H / nsy rounded down or up
+  st.y0 = (int)((long long)sy * a.H / a.nsy);
+  st.rown = (int)((long long)(sy + 1) * a.H / a.nsy) - st.y0;
   st.lane = lane;
   st.col = x0 - 2 + lane;
   st.cc = min(max(st.col, 0), a.W - 1);
@@ -830,14 +837,24 @@ __global__ __launch_bounds__(256, USF_PHOTO_WAVES) void photo_strip_kernel(Strip
   st.template load_flow<0>(st.y0 - 2, true);
   st.template load_flow<1>(st.y0 - 1, true);
   st.template issue<0>(st.y0 - 2, true);
-  int i = 0;
-  for (; i + 3 <= nsteps; i += 3) {
-    st.template step<0>(i, nsteps);
-    st.template step<1>(i + 1, nsteps);
-    st.template step<2>(i + 2, nsteps);
+  // steps 0-3: the two halo rows above, then own rows y0, y0 + 1 (if the
+  // strip has them) with the windows above them; no basis completes yet
+  st.template step<0, 0, 0, 0>(0, nsteps);
+  st.template step<1, 0, 0, 0>(1, nsteps);
+  st.template step<2, 2, 2, 0>(2, nsteps);
+  st.template step<0, 2, 2, 0>(3, nsteps);
+  // interior: own row staged, window and basis of the row two above
+  int i = 4;
+  for (; i + 3 <= st.rown + 2; i += 3) {
+    st.template step<1, 1, 1, 1>(i, nsteps);
+    st.template step<2, 1, 1, 1>(i + 1, nsteps);
+    st.template step<0, 1, 1, 1>(i + 2, nsteps);
   }
-  if (i < nsteps) st.template step<0>(i, nsteps);
-  if (i + 1 < nsteps) st.template step<1>(i + 1, nsteps);
+  // tail: up to two interior steps left, then the two halo rows below (at most 4)
+  if (i < nsteps) st.template step<1>(i, nsteps);
+  if (i + 1 < nsteps) st.template step<2>(i + 1, nsteps);
+  if (i + 2 < nsteps) st.template step<0>(i + 2, nsteps);
+  if (i + 3 < nsteps) st.template step<1>(i + 3, nsteps);
 
   // ---- wave partials (fixed-order butterflies), one slot per (direction, sample, strip)
   float l1 = st.l1, ssum = st.ssum, msum = st.msum;
@@ -855,29 +872,38 @@ __global__ __launch_bounds__(256, USF_PHOTO_WAVES) void photo_strip_kernel(Strip
   }
 }
 
-// Own rows per strip: every wave of a launch does the same (R + 4)-step
-// stream, so the launch takes about max(waves per SIMD, 2) x (R + 4) steps
-// (below 2 waves per SIMD a lone wave issues at half rate, so fewer waves no
-// longer help). The smallest such product wins; ties go to the smaller R.
-constexpr int kStripRows[] = {4, 6, 8, 12, 16, 20, 24, 32};
+// Strip heights. Every wave streams R + 4 rows, so a launch takes about
+// (R + 4) steps times the rounds of waves the chip holds: USF_PHOTO_WAVES per
+// SIMD (the kernel's registers), 1024 SIMDs. A step of a wave alone on its
+// SIMD takes ~0.76 of a step with a second wave beside it (measured,
+// profiles/r03_photo_rows.json), so below one wave per SIMD fewer, taller
+// strips do not help. The strips of a column are balanced (heights differ by
+// at most one row); the cheapest count wins, ties to fewer strips.
 constexpr int kSimds = 1024;  // 256 CUs x 4 SIMDs
+constexpr int kMinStripRows = 4;  // the partials buffer holds ceil(H / 4) strips per column
 
-int strip_rows(int B, int H, int W, int ndir) {
+struct StripPlan {
+  int R, nsy;
+};
+
+StripPlan strip_plan(int B, int H, int W, int ndir) {
   static const int forced = [] {  // USF_PHOTO_ROWS=R: tuning override (tools/photoab.py)
     const char* v = getenv("USF_PHOTO_ROWS");
     return v ? atoi(v) : 0;
   }();
-  if (forced >= kStripRows[0]) return forced;  // (partials are sized for R >= 4)
-  const long long nsx = (W + kSO - 1) / kSO;
-  int best = kStripRows[0];
-  long long best_cost = -1;
-  for (int R : kStripRows) {
-    const long long waves = (long long)ndir * B * nsx * ((H + R - 1) / R);
-    const long long per_simd = std::max<long long>((waves + kSimds - 1) / kSimds, 2);
-    const long long cost = per_simd * (std::min(R, H) + 4);
+  if (forced >= kMinStripRows) return {forced, (H + forced - 1) / forced};
+  const long long cols = (long long)ndir * B * ((W + kSO - 1) / kSO);
+  StripPlan best{H, 1};
+  double best_cost = -1.0;
+  for (int nsy = 1; nsy <= (H + kMinStripRows - 1) / kMinStripRows; ++nsy) {
+    const int R = (H + nsy - 1) / nsy;
+    if ((H + R - 1) / R != nsy) continue;  // the same R as a smaller count
+    const long long waves = cols * nsy;
+    const long long rounds = (waves + (long long)USF_PHOTO_WAVES * kSimds - 1) / ((long long)USF_PHOTO_WAVES * kSimds);
+    const double cost = (double)rounds * (R + 4) * (waves > kSimds ? 1.0 : 0.76);
     if (best_cost < 0 || cost < best_cost) {
       best_cost = cost;
-      best = R;
+      best = {R, nsy};
     }
   }
   return best;
@@ -904,9 +930,10 @@ hipError_t photo_strip_launch(const PhotoArgs& a, int ndir, int pad_mode, float*
   sa.B = a.B;
   sa.H = a.H;
   sa.W = a.W;
-  sa.R = strip_rows(a.B, a.H, a.W, ndir);
+  const StripPlan plan = strip_plan(a.B, a.H, a.W, ndir);
+  sa.R = plan.R;
   sa.nsx = (a.W + kSO - 1) / kSO;
-  sa.nsy = (a.H + sa.R - 1) / sa.R;
+  sa.nsy = plan.nsy;
   sa.ndir = ndir;
   sa.nitems = ndir * a.B * sa.nsx * sa.nsy;
   const dim3 grid((unsigned)((sa.nitems + 3) / 4));
@@ -958,7 +985,7 @@ hipError_t photo_launch(const PhotoArgs& a, int ndir, int pad_mode, float* parti
 int photo_partials(int B, int H, int W) {
   // either kernel, any strip height (the smallest R has the most strips)
   const int tile = 3 * B * ((H + kTH - 1) / kTH) * ((W + kTW - 1) / kTW);
-  const int strip = 3 * B * ((H + kStripRows[0] - 1) / kStripRows[0]) * ((W + kSO - 1) / kSO);
+  const int strip = 3 * B * ((H + kMinStripRows - 1) / kMinStripRows) * ((W + kSO - 1) / kSO);
   return std::max(tile, strip);
 }
 

@@ -1,33 +1,34 @@
 // STREAM copy with 16-byte lanes: the device-copy ceiling bench.py reports
 // beside the roofline (MI355X_MICROARCH.md measures 6.29 TB/s with a float4
-// copy; torch's copy_ measured 4.7-5.3 TB/s on the same box). A grid-stride
-// loop over float4s, 4 loads in flight per lane, grid sized to 8 workgroups
-// per CU.
+// copy; torch's copy_ measured 4.6-5.3 TB/s on the same box). One 16 KiB
+// chunk per workgroup, 16-byte nontemporal loads and stores, 4 in flight per
+// lane (a grid-stride form with 8 workgroups per CU measured 4.6 TB/s).
 #include "usf_common.h"
 
 namespace usf {
 namespace {
 
-__global__ __launch_bounds__(256) void stream_copy_kernel(const float4* __restrict__ src, float4* __restrict__ dst,
+using f4 = float __attribute__((ext_vector_type(4)));
+
+__global__ __launch_bounds__(256) void stream_copy_kernel(const f4* __restrict__ src, f4* __restrict__ dst,
                                                           long long n4) {
-  const long long stride = (long long)gridDim.x * 256;
-  long long i = (long long)blockIdx.x * 256 + threadIdx.x;
-  for (; i + 3 * stride < n4; i += 4 * stride) {
-    const float4 a = src[i], b = src[i + stride], c = src[i + 2 * stride], d = src[i + 3 * stride];
-    dst[i] = a;
-    dst[i + stride] = b;
-    dst[i + 2 * stride] = c;
-    dst[i + 3 * stride] = d;
-  }
-  for (; i < n4; i += stride) dst[i] = src[i];
+  // one 16 KiB block-contiguous chunk per workgroup, 4 loads in flight per lane
+  const long long base = (long long)blockIdx.x * 1024 + threadIdx.x;
+  f4 v[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    if (base + 256 * k < n4) v[k] = __builtin_nontemporal_load(src + base + 256 * k);
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    if (base + 256 * k < n4) __builtin_nontemporal_store(v[k], dst + base + 256 * k);
 }
 
 }  // namespace
 
 hipError_t stream_copy_launch(const float* src, float* dst, long long n, hipStream_t s) {
   const long long n4 = n / 4;
-  hipLaunchKernelGGL(stream_copy_kernel, dim3(256 * 8), dim3(256), 0, s, reinterpret_cast<const float4*>(src),
-                     reinterpret_cast<float4*>(dst), n4);
+  hipLaunchKernelGGL(stream_copy_kernel, dim3((unsigned)((n4 + 1023) / 1024)), dim3(256), 0, s,
+                     reinterpret_cast<const f4*>(src), reinterpret_cast<f4*>(dst), n4);
   return hipGetLastError();
 }
 

@@ -496,8 +496,9 @@ __global__ __launch_bounds__(256) void warp_gx_bins_kernel(const float* __restri
   // (W % 4 == 0): every box quad is then one aligned 16-byte load inside its row
   const bool w4 = (W & 3) == 0;
   const int by0 = bb[0], bx0 = w4 ? bb[2] & ~3 : bb[2];
-  const int bh = bb[1] - by0 + 1, bw = bb[3] - bx0 + 1;
-  const bool staged = bb[0] <= bb[1] && bh <= kBoxH && bw <= kBoxW;  // workgroup-uniform
+  const bool any = bb[0] <= bb[1];  // no entry in the workgroup: bb keeps INT_MAX / INT_MIN
+  const int bh = any ? bb[1] - by0 + 1 : 0, bw = any ? bb[3] - bx0 + 1 : 0;  // (no signed overflow)
+  const bool staged = any && bh <= kBoxH && bw <= kBoxW;  // workgroup-uniform
   const float* gb = gout + (size_t)b * C * HW;
   float* gq = gx + (size_t)b * C * HW + qq;
   // per entry: offset into the staged box, or the plane offset
@@ -1019,13 +1020,20 @@ void bwd_gather_cs(const float* x, const float* flow, long long fbs, const float
 // tests/test_gpu_graph_replay.py), so every fill the library needs is this
 // launch, ordered like its other kernels in eager and captured streams alike.
 // p 16-byte aligned (torch allocations, the workspace layout), bytes % 4 == 0.
-__global__ __launch_bounds__(256) void zero_fill_kernel(unsigned* __restrict__ p, long long n) {
+// 16-byte stores from the first 16-byte boundary on; the dwords before it (a
+// caller pointer through the C ABI need only be 4-byte aligned) and the tail
+// are stored singly.
+__global__ __launch_bounds__(256) void zero_fill_kernel(unsigned* __restrict__ p, long long n, int head) {
+  const long long t = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (t < head && t < n) p[t] = 0u;
+  unsigned* q = p + head;
+  const long long m = n - head;
   const long long stride = (long long)gridDim.x * 256 * 4;
-  for (long long i = ((long long)blockIdx.x * 256 + threadIdx.x) * 4; i < n; i += stride) {
-    if (i + 4 <= n) {
-      *reinterpret_cast<uint4*>(p + i) = make_uint4(0u, 0u, 0u, 0u);
+  for (long long i = t * 4; i < m; i += stride) {
+    if (i + 4 <= m) {
+      *reinterpret_cast<uint4*>(q + i) = make_uint4(0u, 0u, 0u, 0u);
     } else {
-      for (long long j = i; j < n; ++j) p[j] = 0u;
+      for (long long j = i; j < m; ++j) q[j] = 0u;
     }
   }
 }
@@ -1033,8 +1041,10 @@ __global__ __launch_bounds__(256) void zero_fill_kernel(unsigned* __restrict__ p
 hipError_t zero_fill(void* p, size_t bytes, hipStream_t s) {
   const long long n = (long long)(bytes / 4);
   if (n <= 0) return hipSuccess;
+  const int head = (int)std::min<long long>(((16 - (reinterpret_cast<uintptr_t>(p) & 15)) & 15) / 4, n);
   const long long blocks = std::min<long long>((n + 1023) / 1024, 4096);
-  hipLaunchKernelGGL(zero_fill_kernel, dim3((unsigned)blocks), dim3(256), 0, s, static_cast<unsigned*>(p), n);
+  hipLaunchKernelGGL(zero_fill_kernel, dim3((unsigned)blocks), dim3(256), 0, s, static_cast<unsigned*>(p), n,
+                     head);
   return hipGetLastError();
 }
 
