@@ -42,7 +42,9 @@ def selected_sites():
 
 
 def main():
-    _lib.load()
+    lib = _lib.load()
+    if os.environ.get("USF_PHOTO_VARIANT"):  # photometric kernel A/B (usf_set_variant op 3)
+        lib.usf_set_variant(3, int(os.environ["USF_PHOTO_VARIANT"]))
     dev = torch.device("cuda:0")
     n = int(os.environ.get("KPROF_N", "3"))
     # calibration: a plain 256 MiB device copy (16-B loads/stores) for FETCH/WRITE_SIZE scaling

@@ -872,6 +872,338 @@ __global__ __launch_bounds__(256, USF_PHOTO_WAVES) void photo_strip_kernel(Strip
   }
 }
 
+// ------------------------------------------------ producer / consumer pair --
+// photo_pc_kernel: the strip stream of photo_strip_kernel split over a PAIR of
+// waves, so each holds half the state and twice as many waves share a SIMD.
+// The producer stages rows (flow, tap, gathers, x = rec m, y = tgt m, the L1
+// and mask sums, its own pixels' dI/dflow and the A basis) and hands each row's
+// x, y and {dix kx, diy ky} to the consumer through an LDS ring; the consumer
+// turns them into row sums, windows (SSIM and its coefficients) and the S
+// basis, one row behind. One workgroup barrier per step: the producer writes
+// row t while the consumer reads rows t-1 (new) and t-3 (the pixel row whose
+// basis completes), so a ring of 4 rows suffices. Both pairs of a workgroup
+// stream the same strip rows (the two directions, or two neighbouring strips),
+// so they take the same number of steps and barriers.
+constexpr int kRing = 4;
+
+template <bool BORDER, bool GRAD, int C>
+struct PairCommon {
+  __amdgpu_buffer_rsrc_t rbas;
+  int H, W, HW, y0, rown, col, cc, lane;
+  bool col_in, lane_own, wcol;
+  float* xy;  // this pair's LDS ring: [kRing][C][2][64] (x, y planes)
+  float* pd;  // [kRing][C][2][64] (dix kx, diy ky planes)
+  __device__ __forceinline__ void st(float v, int off, int soff) {
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(int, v), rbas, off, soff, 0);
+  }
+  __device__ __forceinline__ int ring(int slot, int c, int k) const { return ((slot * C + c) * 2 + k) * 64 + lane; }
+};
+
+template <bool BORDER, bool GRAD, int C>
+struct Producer : PairCommon<BORDER, GRAD, C> {
+  using B_ = PairCommon<BORDER, GRAD, C>;
+  __amdgpu_buffer_rsrc_t rs[C], rflow, rmask, rtgt;
+  float fxs, fys;
+  float fu[3], fv[3];
+  float gv[3][C][4], tt[3][C], mm[3];
+  float tn[3], tw[3], tmx[3], tmy[3];
+  float l1, msum;
+
+  __device__ __forceinline__ static float ld(__amdgpu_buffer_rsrc_t r, int off, int soff) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, soff, 0));
+  }
+  __device__ __forceinline__ int row_off(int r, bool ok) const {
+    return ok && r >= 0 && r < this->H ? 4 * (r * this->W + this->cc) : kOffNone;
+  }
+  template <int slot>
+  __device__ __forceinline__ void load_flow(int r, bool ok) {
+    const int o = row_off(r, ok);
+    fu[slot] = ld(rflow, o, 0);
+    fv[slot] = ld(rflow, o, 4 * this->HW);
+  }
+  template <int slot>
+  __device__ __forceinline__ void issue(int r, bool ok) {
+    const TapB tp = make_tap_b<BORDER>(fu[slot], fv[slot], this->cc, r, this->H, this->W);
+    const int o = row_off(r, ok);
+    const bool in = o != kOffNone;
+    const int onw = in ? tp.onw : kOffNone, one = in ? tp.one : kOffNone;
+    const int osw = in ? tp.osw : kOffNone, ose = in ? tp.ose : kOffNone;
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      gv[slot][c][0] = ld(rs[c], onw, 0);
+      gv[slot][c][1] = ld(rs[c], one, 0);
+      gv[slot][c][2] = ld(rs[c], osw, 0);
+      gv[slot][c][3] = ld(rs[c], ose, 0);
+      tt[slot][c] = ld(rtgt, o, 4 * c * this->HW);
+    }
+    mm[slot] = ld(rmask, o, 0);
+    tn[slot] = tp.n;
+    tw[slot] = tp.w;
+    tmx[slot] = tp.mx;
+    tmy[slot] = tp.my;
+  }
+  // row r = y0 - 2 + i; ST: own row (0 / 1 / 2 = run time); ends with the step's barrier
+  template <int PH, int ST>
+  __device__ __forceinline__ void step(int i, int nsteps) {
+    constexpr int S0 = PH, S1 = (PH + 2) % 3, S2 = (PH + 1) % 3;
+    const int r = this->y0 - 2 + i;
+    load_flow<S1>(r + 2, i + 2 < nsteps);
+    issue<S2>(r + 1, i + 1 < nsteps);
+    const bool own_row = ST == 2 ? (i >= 2 && i < this->rown + 2) : ST == 1;
+    const float n = tn[S0], w = tw[S0];
+    float s, e;
+    {
+#pragma clang fp contract(off)
+      s = 1.0f - n;
+      e = 1.0f - w;
+    }
+    const float (&v)[C][4] = gv[S0];
+    const float m = mm[S0];
+    const float me = this->col_in ? m : 0.f;
+    float rec[C], x[C], y[C];
+    {
+#pragma clang fp contract(off)
+      const float wnw = s * e, wne = s * w, wsw = n * e, wse = n * w;
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        rec[c] = v[c][0] * wnw + v[c][1] * wne + v[c][2] * wsw + v[c][3] * wse;
+        x[c] = rec[c] * me;
+        y[c] = tt[S0][c] * me;
+      }
+    }
+    float ax = 0.f, ay = 0.f, kx = 0.f, ky = 0.f;
+    float dk[C][2];
+#pragma unroll
+    for (int c = 0; c < C; ++c) dk[c][0] = dk[c][1] = 0.f;
+    if (own_row) {
+      const float mo = this->lane_own ? m : 0.f;
+      kx = m * tmx[S0] * fxs;
+      ky = m * tmy[S0] * fys;
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        const float diff = rec[c] - tt[S0][c];
+        l1 += fabsf(diff) * mo;
+        if constexpr (GRAD) {
+          const float dix = (v[c][1] - v[c][0]) * s + (v[c][3] - v[c][2]) * n;
+          const float diy = (v[c][2] - v[c][0]) * e + (v[c][3] - v[c][1]) * w;
+          const float sg = diff > 0.f ? 1.f : (diff < 0.f ? -1.f : 0.f);
+          ax += sg * dix;
+          ay += sg * diy;
+          dk[c][0] = dix * kx;
+          dk[c][1] = diy * ky;
+        }
+      }
+      msum += mo;
+    }
+    const int slot = i & (kRing - 1);
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      this->xy[this->ring(slot, c, 0)] = x[c];
+      this->xy[this->ring(slot, c, 1)] = y[c];
+      if constexpr (GRAD) {
+        this->pd[this->ring(slot, c, 0)] = dk[c][0];
+        this->pd[this->ring(slot, c, 1)] = dk[c][1];
+      }
+    }
+    if constexpr (GRAD) {
+      const int o = own_row && this->lane_own ? 4 * (r * this->W + this->col) : kOffNone;
+      this->st(ax * kx, o, 0);
+      this->st(ay * ky, o, 4 * this->HW);
+    }
+    __syncthreads();
+  }
+};
+
+template <bool BORDER, bool GRAD, int C>
+struct Consumer : PairCommon<BORDER, GRAD, C> {
+  Sums sm[3][C];
+  float ca[3][C], cb[3][C], cg[3][C];
+  float ssum;
+  // row j of the strip (r = y0 - 2 + j), written by the producer one step
+  // earlier; WIN: window row r - 2; BAS: pixel row r - 2's basis (0 / 1 / 2 =
+  // run time); ends with the step's barrier
+  template <int PH, int WIN, int BAS>
+  __device__ __forceinline__ void step(int j) {
+    constexpr int S0 = PH, S1 = (PH + 2) % 3, S2 = (PH + 1) % 3;
+    const int r = this->y0 - 2 + j;
+    const int slot = j & (kRing - 1), slot2 = (j - 2) & (kRing - 1);
+    float x[C], y[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      x[c] = this->xy[this->ring(slot, c, 0)];
+      y[c] = this->xy[this->ring(slot, c, 1)];
+    }
+#pragma unroll
+    for (int c = 0; c < C; ++c)
+      sm[S0][c] = Sums{hsum_next(x[c]), hsum_next(y[c]), hsum_next(fmaf(x[c], x[c], y[c] * y[c])),
+                       hsum_next(x[c] * y[c])};
+    const int q = r - 2;
+    const bool qown = BAS == 2 ? j >= 4 : BAS == 1;
+    float px[C], py[C], dx[C], dy[C];  // pixel row q: x, y and its gradient state
+    if constexpr (GRAD) {
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        px[c] = this->xy[this->ring(slot2, c, 0)];
+        py[c] = this->xy[this->ring(slot2, c, 1)];
+        dx[c] = this->pd[this->ring(slot2, c, 0)];
+        dy[c] = this->pd[this->ring(slot2, c, 1)];
+      }
+    }
+    float bx = 0.f, by = 0.f;
+    if (WIN == 2 ? j >= 2 : WIN == 1) {
+      const bool wrow = WIN == 1 || (q >= 0 && q <= this->H - 3);
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        float al = 0.f, be = 0.f, ga = 0.f;
+        if (wrow) {
+          const Sums& a2 = sm[S2][c];
+          const Sums& a1 = sm[S1][c];
+          const Sums& a0 = sm[S0][c];
+          const Sums w{a2.x + a1.x + a0.x, a2.y + a1.y + a0.y, a2.q + a1.q + a0.q, a2.xy + a1.xy + a0.xy};
+          const float s = ssim_sums<GRAD>(w, al, be, ga);
+          ssum += qown && this->lane_own && this->wcol ? s : 0.f;
+          if (!this->wcol) al = be = ga = 0.f;
+        }
+        if constexpr (GRAD) {
+          ca[S0][c] = al;
+          cb[S0][c] = be;
+          cg[S0][c] = ga;
+          if (qown) {
+            const float ha = hsum_prev(ca[S2][c] + ca[S1][c] + al);
+            const float hb = hsum_prev(cb[S2][c] + cb[S1][c] + be);
+            const float hg = hsum_prev(cg[S2][c] + cg[S1][c] + ga);
+            const float ds = fmaf(hg, py[c], fmaf(hb, px[c], ha));
+            bx = fmaf(ds, dx[c], bx);
+            by = fmaf(ds, dy[c], by);
+          }
+        }
+      }
+    }
+    if constexpr (GRAD) {
+      const int o = qown && this->lane_own ? 4 * (q * this->W + this->col) : kOffNone;
+      this->st(bx, o, 8 * this->HW);
+      this->st(by, o, 12 * this->HW);
+    }
+    __syncthreads();
+  }
+};
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int s = 32; s > 0; s >>= 1) v += __shfl_xor(v, s);
+  return v;
+}
+
+template <bool BORDER, bool GRAD, int C>
+__global__ __launch_bounds__(256) void photo_pc_kernel(StripArgs a, float* __restrict__ partials) {
+  __shared__ float lds[2][2][kRing * C * 2 * 64];  // [pair][x,y | gradient state]
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int pair = wave >> 1;
+  const bool prod = (wave & 1) == 0;
+  // workgroup -> (sample, strip row, pair of strip items sharing that row)
+  const int npx = a.ndir == 2 ? a.nsx : (a.nsx + 1) / 2;  // workgroups per strip row
+  const int g = xcd_remap(blockIdx.x, gridDim.x);
+  const int gx = g % npx, rest = g / npx;
+  const int sy = rest % a.nsy, b = rest / a.nsy;
+  const int dirn = a.ndir == 2 ? pair : 0;
+  const int sx = a.ndir == 2 ? gx : 2 * gx + pair;
+  const bool valid = sx < a.nsx;  // wave-uniform
+  const int H = a.H, W = a.W;
+  const int y0 = (int)((long long)sy * H / a.nsy);
+  const int rown = (int)((long long)(sy + 1) * H / a.nsy) - y0;
+  const int nsteps = rown + 4;  // the same for both pairs (same strip row)
+  if (!valid) {  // keep the barrier count of the other pair
+    for (int i = 0; i <= nsteps; ++i) __syncthreads();
+    return;
+  }
+  const PhotoDir dr = a.dir[dirn];
+  const int HW = H * W;
+  const size_t HWs = (size_t)HW;
+  const int x0 = sx * kSO;
+  auto init = [&](PairCommon<BORDER, GRAD, C>& p) {
+    p.H = H;
+    p.W = W;
+    p.HW = HW;
+    p.y0 = y0;
+    p.rown = rown;
+    p.lane = lane;
+    p.col = x0 - 2 + lane;
+    p.cc = min(max(p.col, 0), W - 1);
+    p.col_in = p.col >= 0 && p.col < W;
+    p.lane_own = lane >= 2 && lane < 2 + kSO && p.col < W;
+    p.wcol = p.col >= 0 && p.col <= W - 3;
+    p.xy = lds[pair][0];
+    p.pd = lds[pair][1];
+    if constexpr (GRAD) p.rbas = __builtin_amdgcn_make_buffer_rsrc(dr.basis + b * a.bbs, 0, 16 * HW, kRsrcWord3);
+  };
+  float* po = partials + 3 * (((size_t)dirn * a.B + b) * a.nsy * a.nsx + (size_t)sy * a.nsx + sx);
+  if (prod) {
+    Producer<BORDER, GRAD, C> P;
+    init(P);
+    const float* srcb = dr.src + (size_t)b * C * HWs;
+#pragma unroll
+    for (int c = 0; c < C; ++c)
+      P.rs[c] = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(srcb + c * HWs), 0, 4 * HW, kRsrcWord3);
+    P.rtgt = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(dr.tgt + (size_t)b * C * HWs), 0, 4 * C * HW,
+                                               kRsrcWord3);
+    P.rmask = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(dr.mask + (size_t)b * HWs), 0, 4 * HW, kRsrcWord3);
+    P.rflow = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(dr.flow + b * a.fbs), 0, 8 * HW, kRsrcWord3);
+    P.fxs = 2.0f / (float)(W - 1);
+    P.fys = 2.0f / (float)(H - 1);
+    P.l1 = P.msum = 0.f;
+    P.template load_flow<0>(y0 - 2, true);
+    P.template load_flow<1>(y0 - 1, true);
+    P.template issue<0>(y0 - 2, true);
+    P.template step<0, 0>(0, nsteps);
+    P.template step<1, 0>(1, nsteps);
+    int i = 2;
+    for (; i + 3 <= rown + 2; i += 3) {
+      P.template step<2, 1>(i, nsteps);
+      P.template step<0, 1>(i + 1, nsteps);
+      P.template step<1, 1>(i + 2, nsteps);
+    }
+    if (i < nsteps) P.template step<2, 2>(i, nsteps);
+    if (i + 1 < nsteps) P.template step<0, 2>(i + 1, nsteps);
+    if (i + 2 < nsteps) P.template step<1, 2>(i + 2, nsteps);
+    if (i + 3 < nsteps) P.template step<2, 2>(i + 3, nsteps);
+    __syncthreads();  // the consumer's last step
+    const float l1 = wave_sum(P.l1), ms = wave_sum(P.msum);
+    if (lane == 0) {
+      po[0] = l1;
+      po[2] = ms;
+    }
+  } else {
+    Consumer<BORDER, GRAD, C> Q;
+    init(Q);
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        Q.sm[k][c] = Sums{0.f, 0.f, 0.f, 0.f};
+        Q.ca[k][c] = Q.cb[k][c] = Q.cg[k][c] = 0.f;
+      }
+    Q.ssum = 0.f;
+    __syncthreads();  // the producer's first row
+    Q.template step<0, 0, 0>(0);
+    Q.template step<1, 0, 0>(1);
+    Q.template step<2, 2, 0>(2);
+    Q.template step<0, 2, 0>(3);
+    int j = 4;
+    for (; j + 3 <= rown + 2; j += 3) {
+      Q.template step<1, 1, 1>(j);
+      Q.template step<2, 1, 1>(j + 1);
+      Q.template step<0, 1, 1>(j + 2);
+    }
+    if (j < nsteps) Q.template step<1, 2, 2>(j);
+    if (j + 1 < nsteps) Q.template step<2, 2, 2>(j + 1);
+    if (j + 2 < nsteps) Q.template step<0, 2, 2>(j + 2);
+    if (j + 3 < nsteps) Q.template step<1, 2, 2>(j + 3);
+    const float ss = wave_sum(Q.ssum);
+    if (lane == 0) po[1] = ss;
+  }
+}
+
 // Strip heights. Every wave streams R + 4 rows, so a launch takes about
 // (R + 4) steps times the rounds of waves the chip holds: USF_PHOTO_WAVES per
 // SIMD (the kernel's registers), 1024 SIMDs. A step of a wave alone on its
@@ -919,6 +1251,16 @@ hipError_t strip_launch_c(const StripArgs& sa, int C, dim3 grid, float* partials
     hipLaunchKernelGGL((photo_strip_kernel<BORDER, GRAD, 1>), grid, dim3(256), 0, s, sa, partials);
   return hipGetLastError();
 }
+template <bool BORDER, bool GRAD>
+hipError_t pc_launch_c(const StripArgs& sa, int C, dim3 grid, float* partials, hipStream_t s) {
+  if (C == 3)
+    hipLaunchKernelGGL((photo_pc_kernel<BORDER, GRAD, 3>), grid, dim3(256), 0, s, sa, partials);
+  else if (C == 2)
+    hipLaunchKernelGGL((photo_pc_kernel<BORDER, GRAD, 2>), grid, dim3(256), 0, s, sa, partials);
+  else
+    hipLaunchKernelGGL((photo_pc_kernel<BORDER, GRAD, 1>), grid, dim3(256), 0, s, sa, partials);
+  return hipGetLastError();
+}
 
 hipError_t photo_strip_launch(const PhotoArgs& a, int ndir, int pad_mode, float* partials, float* out,
                               float w_l1, float w_ssim, hipStream_t s) {
@@ -936,13 +1278,22 @@ hipError_t photo_strip_launch(const PhotoArgs& a, int ndir, int pad_mode, float*
   sa.nsy = plan.nsy;
   sa.ndir = ndir;
   sa.nitems = ndir * a.B * sa.nsx * sa.nsy;
-  const dim3 grid((unsigned)((sa.nitems + 3) / 4));
   const bool grad = a.dir[0].basis != nullptr;
   hipError_t e;
-  if (pad_mode == 1)
-    e = grad ? strip_launch_c<true, true>(sa, a.C, grid, partials, s) : strip_launch_c<true, false>(sa, a.C, grid, partials, s);
-  else
-    e = grad ? strip_launch_c<false, true>(sa, a.C, grid, partials, s) : strip_launch_c<false, false>(sa, a.C, grid, partials, s);
+  if (variant_override(3) == 2) {  // one wave per strip
+    const dim3 grid((unsigned)((sa.nitems + 3) / 4));
+    if (pad_mode == 1)
+      e = grad ? strip_launch_c<true, true>(sa, a.C, grid, partials, s) : strip_launch_c<true, false>(sa, a.C, grid, partials, s);
+    else
+      e = grad ? strip_launch_c<false, true>(sa, a.C, grid, partials, s) : strip_launch_c<false, false>(sa, a.C, grid, partials, s);
+  } else {  // a producer / consumer pair of waves per strip, two strips per workgroup
+    const int npx = ndir == 2 ? sa.nsx : (sa.nsx + 1) / 2;
+    const dim3 grid((unsigned)(a.B * sa.nsy * npx));
+    if (pad_mode == 1)
+      e = grad ? pc_launch_c<true, true>(sa, a.C, grid, partials, s) : pc_launch_c<true, false>(sa, a.C, grid, partials, s);
+    else
+      e = grad ? pc_launch_c<false, true>(sa, a.C, grid, partials, s) : pc_launch_c<false, false>(sa, a.C, grid, partials, s);
+  }
   if (e != hipSuccess) return e;
   const double n1 = (double)a.B * a.C * a.H * a.W;
   const double n2 = (a.H >= 3 && a.W >= 3) ? (double)a.B * a.C * (a.H - 2) * (a.W - 2) : 0.0;
