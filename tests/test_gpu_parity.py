@@ -418,32 +418,51 @@ def test_occlusion_vs_oracle_full_size(hip_device, shape, scale):
     assert abs(float(rel.sum()) - float(cmap_ref.sum())) < 1e-3 * max(1.0, float(cmap_ref.sum()))
 
 
-@pytest.mark.parametrize("shape", [(8, 192, 4, 13), (8, 128, 8, 26), (8, 96, 16, 52), (3, 100, 5, 9)])
-def test_corr_fwd_channel_split_vs_unsplit_and_oracle(hip_device, shape):
-    """Small levels split the forward's channel loop (usf_corr_fwd_workspace > 0):
-    the fixed-order reduction of the group partials matches the unsplit kernel
-    (usf_corr_fwd_f32, no workspace) and the fp64 oracle; with the LeakyReLU
-    epilogue into a concat slice it matches the composition."""
+@pytest.mark.parametrize("shape,split", [((16, 192, 4, 13), False), ((16, 128, 8, 26), False),
+                                         ((8, 96, 16, 52), True), ((3, 100, 5, 9), False),
+                                         ((4, 512, 4, 13), True)])
+def test_corr_fwd_small_and_split_vs_tiled_and_oracle(hip_device, shape, split):
+    """Small levels: the small-image kernel (one workgroup per sample, dy and
+    row block, all channels staged at once; usf_corr_fwd_workspace == 0) or,
+    where its rows do not fit 64 KB of LDS, the channel split with its reduce
+    (workspace > 0). Either matches the tiled kernel (variant 4, <4,4,8,3,8>)
+    and the fp64 oracle; with the LeakyReLU epilogue into a concat slice it
+    matches the composition, and its sign mask equals the tiled kernel's."""
     from unsamflow_amd import _lib, ops
 
     B, C, H, W = shape
     lib = _lib.load()
-    assert lib.usf_corr_fwd_workspace(B, C, H, W, 4) > 0
+    assert (lib.usf_corr_fwd_workspace(B, C, H, W, 4) > 0) == split
     x1 = hashrng.normal(shape, 5 + C)
     x2 = hashrng.normal(shape, 6 + C)
     t1, t2 = _dev(x1, hip_device), _dev(x2, hip_device)
-    split = ops.corr_forward(t1, t2, 4)
-    plain = torch.empty_like(split)
-    rc = lib.usf_corr_fwd_f32(t1.data_ptr(), t2.data_ptr(), plain.data_ptr(), B, C, H, W, 4,
-                              _lib.stream_handle(t1.device))
-    _lib.check(rc, "usf_corr_fwd_f32")
-    ref = corr_forward_np(x1, x2, 4)
-    np.testing.assert_allclose(_np(split), ref, atol=CORR_ATOL, rtol=CORR_RTOL)
-    np.testing.assert_allclose(_np(split), _np(plain), atol=2e-6, rtol=1e-5)
+    small = ops.corr_forward(t1, t2, 4)
     cat = torch.full((B, 81 + 7, H, W), 7.0, device=hip_device)
-    ops.corr_forward_ex(t1, t2, 4, cat[:, 3:84], leaky_slope=0.1)
-    np.testing.assert_allclose(_np(cat[:, 3:84]), _np(torch.nn.functional.leaky_relu(split, 0.1)), atol=0, rtol=0)
+    mask = ops.corr_act_mask(B, H, W, 4, hip_device)
+    ops.corr_forward_ex(t1, t2, 4, cat[:, 3:84], leaky_slope=0.1, act_mask=mask)
+    lib.usf_set_variant(0, 4)
+    try:
+        tiled = ops.corr_forward(t1, t2, 4)
+        tmask = ops.corr_act_mask(B, H, W, 4, hip_device)
+        tcat = torch.empty((B, 81, H, W), device=hip_device)
+        ops.corr_forward_ex(t1, t2, 4, tcat, leaky_slope=0.1, act_mask=tmask)
+    finally:
+        lib.usf_set_variant(0, -1)
+    ref = corr_forward_np(x1, x2, 4)
+    np.testing.assert_allclose(_np(small), ref, atol=CORR_ATOL, rtol=CORR_RTOL)
+    np.testing.assert_allclose(_np(small), _np(tiled), atol=2e-6, rtol=1e-5)
+    np.testing.assert_allclose(_np(cat[:, 3:84]), _np(torch.nn.functional.leaky_relu(small, 0.1)), atol=0, rtol=0)
     assert float(cat[:, :3].min()) == 7.0 and float(cat[:, 84:].max()) == 7.0
+    # the mask bits are the signs of this call's own outputs; the tiled kernel's
+    # differ only where the two sums straddle zero
+    pos = (cat[:, 3:84] > 0).reshape(B, 9, 9, H, W).cpu().numpy()
+    bits = np.zeros((B, 9, H, (W + 3) // 4), np.uint64)
+    for dx in range(9):
+        for x in range(W):
+            bits[..., x // 4] |= pos[:, :, dx, :, x].astype(np.uint64) << np.uint64(4 * dx + x % 4)
+    assert np.array_equal(mask.cpu().numpy().view(np.uint64), bits)
+    tm = tmask.cpu().numpy().view(np.uint64)
+    assert np.mean(tm == bits) > 0.99
 
 
 @pytest.mark.parametrize("shape,scale", [((2, 8, 64, 208), 1.5), ((1, 4, 65, 130), 3.0), ((2, 4, 64, 208), 0.0)])

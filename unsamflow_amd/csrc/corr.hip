@@ -143,6 +143,12 @@ __device__ __forceinline__ float4 buf_load4(__amdgpu_buffer_rsrc_t r, int byte_o
   return make_float4(f.x, f.y, f.z, f.w);
 }
 
+__device__ __forceinline__ unsigned long long buf_load8(__amdgpu_buffer_rsrc_t r, int byte_off) {
+  using u32x2 = unsigned int __attribute__((ext_vector_type(2)));
+  const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(r, byte_off, 0, 0);
+  return (unsigned long long)v.x | ((unsigned long long)v.y << 32);
+}
+
 // LDS read of N consecutive floats with ds_read_b64 (B64) or ds_read_b128.
 template <bool B64, int N>
 __device__ __forceinline__ void lds_read(const float* p, float (&v)[N]) {
@@ -588,6 +594,232 @@ hipError_t launch_fwd(const float* x1, const float* x2, float* out, int B, int C
   return launch_fwd_v<D, PX, SEGX, NDY, CC, 1, CS>(x1, x2, out, B, C, H, W, s, ep);
 }
 
+// ------------------------------------------------------ small-image forward --
+// KITTI L0 / L1 (16 x {192x4x13, 128x8x26} in the decoder): the tiled kernel
+// launches 48 workgroups there and walks 16-24 channel stages, each a full
+// LDS-DMA round trip, so it splits the channel loop over workgroups and adds
+// the partials in a second kernel (two launches, ~17 us). Here one workgroup
+// owns (sample, displacement row dy, image row y) and stages ALL channels
+// of its x1 row and of the x2 row y + dy - d (with the column halo as
+// zeros) at once: one load round trip, one barrier. Thread t computes quad
+// t % Q (4 pixels of one row, all K dx) over the channel slice t / Q; the
+// slices are added through LDS in slice order (so the result is
+// deterministic), and the same workgroup applies the mean, the LeakyReLU
+// epilogue and writes the sign-mask words of its rows.
+// Staging is plain buffer loads + ds_write: W = 13, 26 rows are not 16-byte
+// aligned, and the dword LDS-DMA form moved 64 KB per workgroup at a few
+// bytes per clock (measured: L1 37 us with it vs 18.6 us for the split pair).
+template <int D>
+struct SmallFwdCfg {
+  static constexpr int K = 2 * D + 1;
+  static constexpr int WIN = round_up(4 + 2 * D, 4);  // x2 window of a quad
+  static constexpr int HALO = round_up(2 * D, 4);     // x2 row = 4 W4 + HALO floats
+  static constexpr int NT = 256;
+  static constexpr int LDSN = 8192;                   // 32 KB: 5 workgroups per CU
+  static constexpr int U = 36;                        // loads in flight per thread
+};
+
+// LDS image [C][S] of image row gy, columns gx0 .. gx0 + S - 1, all C
+// channels of one sample, filled by NT2 threads (t = 0 .. NT2-1): element
+// e = t + NT2 u, its column and offset advanced by NT2 with one carry (no
+// divisions in the loop); off-image elements load as zeros (offset past
+// num_records). The workgroup's x1 and x2 images are staged by different
+// waves (descriptors stay wave-uniform), so both are in flight at once.
+// V = 2 (even W, so every column pair is 8-byte aligned and wholly on or off
+// the image): elements are column pairs, one 8-byte load each.
+template <int NT2, int U, int V>
+__device__ __forceinline__ void small_stage(__amdgpu_buffer_rsrc_t rs, float* img, int C, int S, int gy, int gx0,
+                                            int H, int W, int t) {
+  static_assert(V == 1 || V == 2, "dword or dwordx2 elements");
+  const int SV = S / V, n = C * SV, HW = H * W;
+  const int c0 = t / SV;
+  int j = t - c0 * SV;                           // element column (units of V floats)
+  int off = c0 * HW + gy * W + gx0 + V * j;      // float offset (used only on the image)
+  const int dc = NT2 / SV, dj = NT2 - dc * SV;
+  const bool rowok = (unsigned)gy < (unsigned)H;
+  for (int e0 = 0; e0 < n; e0 += NT2 * U) {
+    float v[U][V];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const bool ok = rowok && e0 + u * NT2 + t < n && (unsigned)(gx0 + V * j) < (unsigned)W;
+      if constexpr (V == 1) {
+        v[u][0] = buf_load1(rs, ok ? off * 4 : kOffImage);
+      } else {
+        const unsigned long long w2 = buf_load8(rs, ok ? off * 4 : kOffImage);
+        v[u][0] = __uint_as_float((unsigned)w2);
+        v[u][1] = __uint_as_float((unsigned)(w2 >> 32));
+      }
+      j += dj;
+      off += dc * HW + V * dj;
+      if (j >= SV) { j -= SV; off += HW - S; }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = e0 + u * NT2 + t;
+      if (e < n) {
+        if constexpr (V == 1)
+          img[e] = v[u][0];
+        else
+          reinterpret_cast<float2*>(img)[e] = make_float2(v[u][0], v[u][1]);
+      }
+    }
+  }
+}
+
+template <int D>
+__global__ __launch_bounds__(256) void corr_fwd_small_kernel(const float* __restrict__ x1,
+                                                             const float* __restrict__ x2,
+                                                             float* __restrict__ out, int C, int H,
+                                                             int W, FwdEpi ep) {
+  using F = SmallFwdCfg<D>;
+  constexpr int K = F::K, WIN = F::WIN, NT = F::NT;
+  __shared__ __attribute__((aligned(16))) float sm[F::LDSN];
+  // work item: dy fastest, then row, then sample; the K items of a row (same
+  // x1 row, overlapping x2 rows) run on one XCD
+  const int w = xcd_remap(blockIdx.x, gridDim.x);
+  const int dy = w % K;
+  const int y = (w / K) % H;
+  const int b = w / (K * H);
+  const int W4 = (W + 3) >> 2, S1 = 4 * W4, S2 = 4 * W4 + F::HALO;
+  const int n1 = C * S1;  // x1 image [C][S1], then x2 image [C][S2]
+  const int tid = threadIdx.x;
+  const int HW = H * W;
+  const auto r1 = plane_buf(x1 + (size_t)b * C * HW, C * HW * 4);
+  const auto r2 = plane_buf(x2 + (size_t)b * C * HW, C * HW * 4);
+#if defined(USF_SMALL_PROBE) && USF_SMALL_PROBE == 1
+  if (ep.slope == 12345.f)  // timing probe only: no staging
+#endif
+  if ((W & 1) == 0 && (D & 1) == 0) {  // 8-byte column pairs (x2's halo starts at -D)
+    if (tid < NT / 2)
+      small_stage<NT / 2, F::U / 2, 2>(r1, sm, C, S1, y, 0, H, W, tid);
+    else
+      small_stage<NT / 2, F::U / 2, 2>(r2, sm + n1, C, S2, y + dy - D, -D, H, W, tid - NT / 2);
+  } else {
+    if (tid < NT / 2)
+      small_stage<NT / 2, F::U, 1>(r1, sm, C, S1, y, 0, H, W, tid);
+    else
+      small_stage<NT / 2, F::U, 1>(r2, sm + n1, C, S2, y + dy - D, -D, H, W, tid - NT / 2);
+  }
+  __syncthreads();
+
+  const int Q = W4;  // quads of the row (<= 64, host-checked)
+  // channel slices: as many as the threads allow and whose partials fit the stage
+  const int NS = min(NT / Q, F::LDSN / (K * 4 * Q));
+  const int cs = (C + NS - 1) / NS;
+  const int ns = (C + cs - 1) / cs;  // slices that own channels
+  const int qd = tid % Q, s = tid / Q;
+#if defined(USF_SMALL_PROBE) && USF_SMALL_PROBE == 2
+  if (ep.slope != 12345.f) return;  // timing probe only: staging alone
+#endif
+  float acc[K][4];
+#pragma unroll
+  for (int dx = 0; dx < K; ++dx)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[dx][i] = 0.f;
+  if (s < ns) {
+    const int c1 = min(C, (s + 1) * cs);
+    const float* p1 = sm + 4 * qd;
+    const float* p2 = sm + n1 + 4 * qd;
+#pragma unroll 2
+    for (int c = s * cs; c < c1; ++c) {
+      float a[4], wv[WIN];
+      lds_read<false>(p1 + c * S1, a);
+      lds_read<false>(p2 + c * S2, wv);
+#pragma unroll
+      for (int dx = 0; dx < K; ++dx)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[dx][i] = fmaf(a[i], wv[i + dx], acc[dx][i]);
+    }
+  }
+  __syncthreads();  // staging images free: slice partials [s][dx * 4 + i][Q]
+#if defined(USF_SMALL_PROBE) && USF_SMALL_PROBE == 3
+  if (ep.slope != 12345.f) {  // timing probe only: staging + compute (acc kept live)
+    float t = 0.f;
+#pragma unroll
+    for (int dx = 0; dx < K; ++dx)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) t += acc[dx][i];
+    if (t == 12345.f) out[tid] = t;
+    return;
+  }
+#endif
+  float* red = sm;
+  if (s < ns) {
+#pragma unroll
+    for (int dx = 0; dx < K; ++dx)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) red[(s * (K * 4) + dx * 4 + i) * Q + qd] = acc[dx][i];
+  }
+  __syncthreads();
+
+  const float cf = (float)C, inv = 1.f / cf;
+  const bool pow2 = (C & (C - 1)) == 0;  // acc * (1/C) is then the same number as acc / C
+  const bool leaky = ep.act != 0;
+  const int ss = K * 4 * Q;  // slice stride of the partials
+  for (int o = tid; o < K * S1; o += NT) {
+    const int dx = o / S1, x = o - dx * S1;
+    const int idx = (dx * 4 + (x & 3)) * Q + (x >> 2);
+    // slices added in a fixed order: four interleaved chains, then (0+1)+(2+3)
+    float t[4] = {0.f, 0.f, 0.f, 0.f};
+    int s2 = 0;
+#if defined(USF_SMALL_PROBE) && USF_SMALL_PROBE == 4
+    if (ep.slope == 12345.f)  // timing probe only: no slice sums
+#endif
+    for (; s2 + 4 <= ns; s2 += 4) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) t[k] += red[(s2 + k) * ss + idx];
+    }
+    for (int k = 0; s2 < ns; ++s2, ++k) t[k] += red[s2 * ss + idx];
+    const float sum = (t[0] + t[1]) + (t[2] + t[3]);
+    const float m = pow2 ? sum * inv : sum / cf;
+    const float v = leaky ? (m > 0.f ? m : m * ep.slope) : m;
+    red[idx] = v;  // for the sign mask (this thread is the only reader of idx)
+    if (x < W) out[(size_t)b * ep.out_bstride + (size_t)(dy * K + dx) * HW + y * W + x] = v;
+  }
+  if (!(leaky && ep.mask)) return;
+#if defined(USF_SMALL_PROBE) && USF_SMALL_PROBE == 5
+  if (ep.slope != 12345.f) return;  // timing probe only: no sign mask
+#endif
+  __syncthreads();
+  if (tid < Q) {
+    // all K * 4 reads issued at once (a per-element column test here made them
+    // a dependent chain: ~2-3 us of the kernel), then the columns past W masked
+    float v[K * 4];
+#pragma unroll
+    for (int k = 0; k < K * 4; ++k) v[k] = red[k * Q + tid];
+    unsigned long long bits = 0;
+#pragma unroll
+    for (int k = 0; k < K * 4; ++k) bits |= (unsigned long long)(v[k] > 0.f) << (4 * (k >> 2) + (k & 3));
+    constexpr unsigned long long kRep = [] {
+      unsigned long long r = 0;
+      for (int dx = 0; dx < K; ++dx) r |= 1ull << (4 * dx);
+      return r;
+    }();
+    const int nv = W - 4 * tid;  // valid columns of the quad (> 0)
+    ep.mask[((size_t)(b * K + dy) * H + y) * W4 + tid] = nv >= 4 ? bits : bits & (kRep * ((1ull << nv) - 1));
+  }
+}
+
+// The small-image forward applies where one row of all channels (x1 [C][4 W4]
+// + x2 [C][4 W4 + halo]) fits the 32 KB stage and every slice has a partial slot.
+template <int D>
+bool small_fwd_fits(int C, int H, int W) {
+  using F = SmallFwdCfg<D>;
+  const long W4 = (W + 3) / 4;
+  return (long)C * (8 * W4 + F::HALO) <= F::LDSN && W4 <= 64 && H >= 1;
+}
+
+template <int D>
+hipError_t launch_fwd_small(const float* x1, const float* x2, float* out, int B, int C, int H, int W,
+                            hipStream_t s, FwdEpi ep) {
+  if (!small_fwd_fits<D>(C, H, W)) return hipErrorInvalidValue;
+  ep.groups = 1;
+  ep.part = nullptr;
+  hipLaunchKernelGGL((corr_fwd_small_kernel<D>), dim3((unsigned)(B * H * (2 * D + 1))),
+                     dim3(SmallFwdCfg<D>::NT), 0, s, x1, x2, out, C, H, W, ep);
+  return hipGetLastError();
+}
+
 // Tuning hook: usf_set_variant(0, i) forces candidate i for d=4
 // (tools/kbench.py sweeps them on the GPU); -1 = the shape heuristic below.
 hipError_t fwd_candidate_d4(int i, const float* x1, const float* x2, float* out, int B, int C,
@@ -605,10 +837,11 @@ hipError_t fwd_candidate_d4(int i, const float* x1, const float* x2, float* out,
     case 9: return launch_fwd<4, 4, 8, 3, 4, 2>(x1, x2, out, B, C, H, W, s, ep);
     case 10: return launch_fwd<4, 4, 8, 1, 8, 2>(x1, x2, out, B, C, H, W, s, ep);
     case 11: return launch_fwd<4, 4, 8, 1, 8, 4>(x1, x2, out, B, C, H, W, s, ep);
+    case 12: return launch_fwd_small<4>(x1, x2, out, B, C, H, W, s, ep);
     default: return hipErrorInvalidValue;
   }
 }
-constexpr int kFwdCandidates = 12;
+constexpr int kFwdCandidates = 13;
 
 // Shape heuristic: all displacement rows in one workgroup (x1/x2 staged once)
 // when that still fills the 256 CUs; else split displacement rows across
@@ -618,9 +851,14 @@ constexpr int kFwdCandidates = 12;
 // round trip each) also split the channel loop over `groups` workgroups
 // (>= 2 stages each) when the caller provides the workspace for the partials.
 struct FwdPlan {
-  int cfg;     // 0: <4,8,K,4>, 1: <4,8,K,8>, 2: <4,8,3,8>
+  int cfg;     // 0: <4,8,K,4>, 1: <4,8,K,8>, 2: <4,8,3,8>, 3: small-image kernel
   int groups;  // channel groups
 };
+// the small-image kernel replaces the channel split wherever its rows fit
+// (tools/ab_build.py -DUSF_FWD_SMALL=0: the split + reduce pair)
+#ifndef USF_FWD_SMALL
+#define USF_FWD_SMALL 1
+#endif
 template <int D>
 FwdPlan fwd_plan(int B, int C, int H, int W) {
   constexpr int K = 2 * D + 1;
@@ -643,6 +881,7 @@ FwdPlan fwd_plan(int B, int C, int H, int W) {
       const int CC = 8;
       int g = (int)((USF_FWD_SPLIT_TARGET + wgs - 1) / wgs);
       p.groups = std::max(1, std::min(g, C / (2 * CC)));
+      if (USF_FWD_SMALL && small_fwd_fits<D>(C, H, W)) p = FwdPlan{3, 1};
     }
   }
   return p;
@@ -657,6 +896,7 @@ hipError_t fwd_dispatch(const float* x1, const float* x2, float* out, int B, int
     if (forced >= 0) return fwd_candidate_d4(forced, x1, x2, out, B, C, H, W, s, ep);
   }
   const FwdPlan p = fwd_plan<D>(B, C, H, W);
+  if (p.cfg == 3) return launch_fwd_small<D>(x1, x2, out, B, C, H, W, s, ep);
   if (p.cfg == 0) return launch_fwd<D, 4, 8, K, 4>(x1, x2, out, B, C, H, W, s, ep);
   if (p.cfg == 1) return launch_fwd<D, 4, 8, K, 8>(x1, x2, out, B, C, H, W, s, ep);
   const long long need = (long long)p.groups * B * K * K * H * W;
@@ -704,11 +944,6 @@ struct BwdCfg {
 
 // One (tile, channel group) of gx1 (G2 == false: from g and x2) or gx2
 // (G2 == true: from g and x1; mirrored indices).
-__device__ __forceinline__ unsigned long long buf_load8(__amdgpu_buffer_rsrc_t r, int byte_off) {
-  using u32x2 = unsigned int __attribute__((ext_vector_type(2)));
-  const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(r, byte_off, 0, 0);
-  return (unsigned long long)v.x | ((unsigned long long)v.y << 32);
-}
 
 // Occupancy target of the backward kernels (see corr_bwd_kernel).
 #ifndef USF_BWD_WAVES_PER_EU
