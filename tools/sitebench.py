@@ -76,10 +76,8 @@ def alg_bytes(op, key):
         return 4 * B * H * W * (2 * C + 3)
     if op == "photo_fwd_grad":
         return 4 * B * H * W * (2 * C + 7)
-    if op == "photo_pair":
-        return 2 * 4 * B * H * W * (2 * C + 3)
-    if op == "photo_pair_grad":
-        return 2 * 4 * B * H * W * (2 * C + 7)
+    if op in ("photo_pair", "photo_pair_grad"):  # each input read once (ops.photometric_loss_pair)
+        return 4 * B * H * W * (2 * C + 4 + 2 + (8 if op == "photo_pair_grad" else 0))
     if op == "occ_bwd":
         return 4 * B * H * W * 3
     if op == "upsample":
