@@ -159,6 +159,9 @@ int usf_warp_fwd_f32(const float* x, const float* flow, long long flow_bstride,
  * gx: [B,C,H,W] or NULL; overwritten (the library zeroes it, then scatters
  *     with fp32 atomics: summation order not fixed). Variant 4 of
  *     usf_set_variant(2, .) gathers instead for sources with |flow| < 2 px.
+ *     Variant 7 (images of at most 256 pixels, H, W >= 2; here and in
+ *     usf_warp_bwd_ex_f32) is a one-launch small-image form: each target cell
+ *     sums its sources in pixel order, deterministic, no atomics, no workspace.
  * gflow: [B,2,H,W] dense or NULL; overwritten, deterministic. */
 int usf_warp_bwd_f32(const float* x, const float* flow, long long flow_bstride,
                      const float* gout, float* gx, float* gflow,
@@ -308,7 +311,8 @@ int usf_stream_copy_f32(const float* src, float* dst, long long n, void* stream)
  * config, op 2 = warp grad_x scatter (0 = wave reduce-by-key + direct global
  * atomics, 1 = LDS-aggregated tiles, 2 / 3 = variant 0 with 4 / 1 channel
  * slices per workgroup, 4 = gather for |flow| < 2 px + scatter for the rest,
- * 5 = scatter over vertically adjacent pixel pairs), op 3 = photometric
+ * 5 = scatter over vertically adjacent pixel pairs, 6 = the binned gather
+ * (needs the workspace), 7 = the small-image kernel where H*W <= 256), op 3 = photometric
  * loss kernel (0 = row-streaming strips on producer / consumer wave pairs,
  * the default; 1 = the workgroup-tile kernel of ABI 5; 2 = row-streaming
  * strips on one wave each; 1 and 2 kept for A/B timing); index -1 restores the built-in choice. Returns the number of

@@ -135,7 +135,7 @@ def test_variant_override_bounds(lib):
     assert lib.usf_set_variant(0, n_fwd) == -1 and b"bad op" in lib.usf_last_error_string()
     assert lib.usf_set_variant(4, 0) == -1
     assert lib.usf_set_variant(3, 1) == 3 and lib.usf_set_variant(3, -1) == 3  # photometric: pair / tile / strip
-    assert lib.usf_set_variant(2, 1) == 7 and lib.usf_set_variant(2, -1) == 7
+    assert lib.usf_set_variant(2, 1) == 8 and lib.usf_set_variant(2, -1) == 8  # warp grad_x: 7 = small image
     assert lib.usf_set_variant(1, n_bwd - 1) == n_bwd
     assert lib.usf_set_variant(1, -1) == n_bwd
 

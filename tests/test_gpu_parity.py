@@ -526,3 +526,74 @@ def test_warp_bwd_plain_entry_is_the_scatter(hip_device):
     rx, rf = warp_backward_np(x, flow, g, "border")
     np.testing.assert_allclose(_np(gx), rx, atol=1e-4, rtol=1e-5)
     np.testing.assert_allclose(_np(gf), rf, atol=1e-4, rtol=1e-5)
+
+
+def _small_fields(B, H, W, kind):
+    yy, xx = np.meshgrid(np.arange(H, dtype=np.float32), np.arange(W, dtype=np.float32), indexing="ij")
+    if kind == "zero":
+        f = np.zeros((2, H, W), np.float32)
+    elif kind == "smooth":
+        f = np.stack([1.7 * np.sin(xx / 3.0) + 0.3, 1.2 * np.cos(yy / 2.0) - 0.4])
+    elif kind == "collapse":  # every pixel lands near one spot: cells with far more than 8 sources
+        f = np.stack([0.95 * ((W - 1) / 2.0 - xx) + 0.3, 0.95 * ((H - 1) / 2.0 - yy) + 0.2])
+    else:  # large random displacements, many off the image
+        return hashrng.symmetric((B, 2, H, W), 733, 6.0)
+    return np.ascontiguousarray(f[None].repeat(B, 0).astype(np.float32))
+
+
+@pytest.mark.parametrize("pad", ["border", "zeros"])
+@pytest.mark.parametrize("kind", ["zero", "smooth", "collapse", "random"])
+@pytest.mark.parametrize("shape", [(4, 128, 8, 26), (3, 5, 7, 9), (2, 3, 16, 16)])
+def test_warp_backward_small_image_vs_oracle(hip_device, shape, kind, pad):
+    """The small-image backward (usf_set_variant(2, 7), images of <= 256
+    pixels): each target cell sums its sources in pixel order. Matches the
+    oracle for smooth, zero, fully contracting (cells with > 8 sources: the
+    pool path) and large random flows; bit-identical across runs; each
+    gradient alone equals its share of the joint call."""
+    from unsamflow_amd import _lib, ops
+
+    lib = _lib.load()
+    lib.usf_set_variant(2, 7)
+    try:
+        _small_image_case(hip_device, shape, kind, pad)
+    finally:
+        lib.usf_set_variant(2, -1)
+
+
+def _small_image_case(hip_device, shape, kind, pad):
+    from unsamflow_amd import ops
+
+    B, C, H, W = shape
+    x = hashrng.uniform(shape, 730 + C)
+    g = hashrng.normal(shape, 731 + C)
+    flow = _small_fields(B, H, W, kind)
+    tx, tf, tg = _dev(x, hip_device), _dev(flow, hip_device), _dev(g, hip_device)
+    gx, gf = ops.warp_backward(tx, tf, tg, pad)
+    rx, rf = warp_backward_np(x, flow, g, pad)
+    np.testing.assert_allclose(_np(gx), rx, atol=1e-4, rtol=1e-5)
+    np.testing.assert_allclose(_np(gf), rf, atol=1e-4, rtol=1e-5)
+    gx2, gf2 = ops.warp_backward(tx, tf, tg, pad)
+    assert torch.equal(gx, gx2) and torch.equal(gf, gf2)
+    ox, _ = ops.warp_backward(tx, tf, tg, pad, need_flow=False)
+    _, of = ops.warp_backward(tx, tf, tg, pad, need_x=False)
+    assert torch.equal(ox, gx) and torch.equal(of, gf)
+
+
+def test_warp_backward_small_image_flow_slice(hip_device):
+    """The loss-style flow slice (batch stride 4HW) through the small-image kernel."""
+    from unsamflow_amd import _lib, ops
+
+    B, C, H, W = 3, 16, 8, 26
+    x = hashrng.uniform((B, C, H, W), 740)
+    g = hashrng.normal((B, C, H, W), 741)
+    f4 = hashrng.symmetric((B, 4, H, W), 742, 2.5)
+    t4 = _dev(f4, hip_device)
+    lib = _lib.load()
+    lib.usf_set_variant(2, 7)
+    try:
+        gx, gf = ops.warp_backward(_dev(x, hip_device), t4[:, 2:], _dev(g, hip_device), "border")
+    finally:
+        lib.usf_set_variant(2, -1)
+    rx, rf = warp_backward_np(x, np.ascontiguousarray(f4[:, 2:]), g, "border")
+    np.testing.assert_allclose(_np(gx), rx, atol=1e-4, rtol=1e-5)
+    np.testing.assert_allclose(_np(gf), rf, atol=1e-4, rtol=1e-5)

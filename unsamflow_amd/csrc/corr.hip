@@ -1423,7 +1423,7 @@ namespace {
 
 static int g_variant[4] = {-1, -1, -1, -1};
 int variant_override(int op) { return __atomic_load_n(&g_variant[op], __ATOMIC_RELAXED); }
-int variant_count(int op) { return op == 0 ? kFwdCandidates : op == 1 ? kBwdCandidates : op == 2 ? 7 : 3; }
+int variant_count(int op) { return op == 0 ? kFwdCandidates : op == 1 ? kBwdCandidates : op == 2 ? 8 : 3; }
 void set_variant_override(int op, int index) { __atomic_store_n(&g_variant[op], index, __ATOMIC_RELAXED); }
 
 hipError_t corr_fwd_launch(const float* x1, const float* x2, float* out, int B, int C, int H,

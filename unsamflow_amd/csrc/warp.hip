@@ -1131,6 +1131,219 @@ void bwd_bins(const float* x, const float* flow, long long fbs, const float* gou
   hipLaunchKernelGGL((warp_gx_ovf_kernel<BORDER>), dim3(256), dim3(256), 0, s, flow, fbs, gout, ba, gx, C, H, W);
 }
 
+// --------------------------------------------------- small-image backward --
+// Decoder level 1 (batch 16 x 128 x 8 x 26: 208 pixels a sample): the binned
+// gather is four launches of a few workgroups each, ~20 us of latency chains.
+// Here ONE launch of two kinds of 1024-thread workgroups does both gradients,
+// deterministically, each workgroup in one load round trip:
+//  * grad_x, one workgroup per (sample, group of kSmallCG channels): it stages
+//    the group's grad_out planes in LDS and computes every pixel's tap (the
+//    reference chain, make_tap). Thread q (< HW) then lists the (pixel, corner)
+//    pairs that land on cell q by scanning the taps in pixel order -- a fixed
+//    summation order with no atomics and no sort -- keeping the first kSmallM
+//    in registers and the rest of a crowded cell in an LDS pool; thread
+//    (cell, slice) sums weight * grad_out over the list for its channels;
+//  * grad_flow, one workgroup per (sample, 64 pixels): thread (pixel, slice)
+//    accumulates its channels' tap derivative terms from direct loads (all in
+//    flight at once), and the 16 slices are added in a fixed order.
+// Opt-in (usf_set_variant(2, 7)): measured slower than the binned gather
+// (profiles/ab_r03/warp_small.json); -DUSF_WARP_SMALL=1 makes it the default
+// where it fits.
+#ifndef USF_WARP_SMALL
+#define USF_WARP_SMALL 0
+#endif
+constexpr int kSmallNT = 1024;
+constexpr int kSmallMaxHW = 256;
+#ifndef USF_WARP_SMALL_CG
+#define USF_WARP_SMALL_CG 32
+#endif
+constexpr int kSmallCG = USF_WARP_SMALL_CG;  // channels per grad_x workgroup
+constexpr int kSmallM = 8;     // list entries a thread keeps in registers
+constexpr int kSmallPool = 4 * kSmallMaxHW;
+constexpr int kSmallLD = (kSmallCG * kSmallMaxHW + kSmallNT - 1) / kSmallNT;  // staged floats per thread
+constexpr int kSmallGFP = 64;  // pixels per grad_flow workgroup (x 16 channel slices)
+
+template <bool BORDER>
+__global__ __launch_bounds__(kSmallNT) void warp_bwd_small_kernel(const float* __restrict__ x,
+                                                                  const float* __restrict__ flow,
+                                                                  long long fbs,
+                                                                  const float* __restrict__ gout,
+                                                                  float* __restrict__ gx,
+                                                                  float* __restrict__ gflow, int B, int C,
+                                                                  int H, int W, int ngx) {
+  __shared__ int4 tof[kSmallMaxHW];    // corner target cells (-1: off the image)
+  __shared__ float4 twt[kSmallMaxHW];  // corner weights (nw, ne, sw, se)
+  __shared__ int ltop;                 // pool fill
+  __shared__ int ext[4];               // corner displacement extents: min/max (xw - x), (yn - y)
+  __shared__ int lcnt[kSmallMaxHW], lbeg[kSmallMaxHW];  // a cell's sources; its pool range
+  __shared__ unsigned short lsp[kSmallM][kSmallMaxHW];  // a cell's first kSmallM source pixels
+  __shared__ float lsw[kSmallM][kSmallMaxHW];           // and their weights
+  __shared__ unsigned short pool[kSmallPool];           // pixel * 4 + corner
+  __shared__ float gst[kSmallCG][kSmallMaxHW];          // the group's grad_out planes
+  __shared__ float red[2][kSmallNT];
+  const int HW = H * W;
+  const int t = threadIdx.x;
+  const bool is_gx = (int)blockIdx.x < ngx;
+  const int wi = is_gx ? blockIdx.x : blockIdx.x - ngx;
+  const float* fb0 = flow;
+
+  if (!is_gx) {  // ---- grad_flow of 64 pixels of one sample (uniform branch)
+    constexpr int NSL = kSmallNT / kSmallGFP;  // 16 channel slices
+    const int nblk = (HW + kSmallGFP - 1) / kSmallGFP;
+    const int b = wi / nblk;
+    const int pp = (wi - b * nblk) * kSmallGFP + (t & (kSmallGFP - 1));
+    const int slice = t / kSmallGFP;
+    const bool pin = pp < HW;
+    const int pc = pin ? pp : 0;
+    const float* fb = fb0 + b * fbs;
+    const Tap tp = make_tap(fb[pc], fb[HW + pc], pc % W, pc / W, H, W, BORDER);
+    const float* xb = x + (size_t)b * C * HW;
+    const float* gb = gout + (size_t)b * C * HW;
+    float dix = 0.f, diy = 0.f;
+    // channels slice, slice + 16, ... in batches of 8: 40 loads in flight
+    constexpr int U = 8;
+    for (int cb = slice; cb < C; cb += NSL * U) {
+      float go[U], vnw[U], vne[U], vsw[U], vse[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int c = cb + NSL * u;
+        const bool ok = pin && c < C;
+        const float* xc = xb + (size_t)(ok ? c : 0) * HW;
+        go[u] = ok ? gb[(size_t)c * HW + pc] : 0.f;
+        vnw[u] = ok && tp.m_nw ? xc[tp.o_nw] : 0.f;
+        vne[u] = ok && tp.m_ne ? xc[tp.o_ne] : 0.f;
+        vsw[u] = ok && tp.m_sw ? xc[tp.o_sw] : 0.f;
+        vse[u] = ok && tp.m_se ? xc[tp.o_se] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (cb + NSL * u < C) {
+          dix += ((vne[u] - vnw[u]) * tp.s + (vse[u] - vsw[u]) * tp.n) * go[u];
+          diy += ((vsw[u] - vnw[u]) * tp.e + (vse[u] - vne[u]) * tp.w) * go[u];
+        }
+      }
+    }
+    red[0][t] = dix;
+    red[1][t] = diy;
+    __syncthreads();
+    if (slice != 0 || !pin) return;
+    for (int k = 1; k < NSL; ++k) {  // slices in a fixed order (deterministic)
+      dix += red[0][t + k * kSmallGFP];
+      diy += red[1][t + k * kSmallGFP];
+    }
+    // grid grad, then norm_grid's autograd (DivBackward by (W-1), MulBackward by 2)
+    const float ggx = dix * tp.mx, ggy = diy * tp.my;
+    float* gf = gflow + (size_t)b * 2 * HW + pp;
+    gf[0] = (ggx / (float)(W - 1)) * 2.0f;
+    gf[HW] = (ggy / (float)(H - 1)) * 2.0f;
+    return;
+  }
+
+  // ---- grad_x of channels [c0, c0 + kSmallCG) of sample b
+  constexpr int NS = kSmallNT / kSmallMaxHW;  // channel slices: thread = (cell, slice)
+  const int G = (C + kSmallCG - 1) / kSmallCG;
+  const int b = wi / G;
+  const int c0 = (wi - b * G) * kSmallCG;
+  const int pp = t % HW, slice = t / HW;
+  const float* gb = gout + (size_t)b * C * HW;
+  float v[kSmallLD];  // the group's grad_out planes, issued before the tap chain
+#pragma unroll
+  for (int u = 0; u < kSmallLD; ++u) {
+    const int e = t + kSmallNT * u, c = e / HW, q = e - c * HW;
+    v[u] = c < kSmallCG && c0 + c < C ? gb[(size_t)(c0 + c) * HW + q] : 0.f;
+  }
+  if (t < 4) ext[t] = (t & 1) ? INT_MIN : INT_MAX;
+  if (t == 0) ltop = 0;
+  __syncthreads();
+  if (t < HW) {
+    const float* fb = fb0 + b * fbs;
+    const Tap tp = make_tap(fb[t], fb[HW + t], t % W, t / W, H, W, BORDER);
+    const int4 o = make_int4(tp.m_nw ? tp.o_nw : -1, tp.m_ne ? tp.o_ne : -1, tp.m_sw ? tp.o_sw : -1,
+                             tp.m_se ? tp.o_se : -1);
+    tof[t] = o;
+    twt[t] = make_float4(tp.s * tp.e, tp.s * tp.w, tp.n * tp.e, tp.n * tp.w);
+    if (o.x >= 0 || o.y >= 0 || o.z >= 0 || o.w >= 0) {  // extents of the pixels that land anywhere
+      const int dxw = tp.xw - t % W, dyn = tp.yn - t / W;
+      atomicMin(&ext[0], dxw);
+      atomicMax(&ext[1], dxw);
+      atomicMin(&ext[2], dyn);
+      atomicMax(&ext[3], dyn);
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < kSmallLD; ++u) {
+    const int e = t + kSmallNT * u, c = e / HW, q = e - c * HW;
+    if (c < kSmallCG) gst[c][q] = v[u];
+  }
+  __syncthreads();
+  // thread q < HW lists the sources of cell q: the pixels whose corner cells
+  // can include q (north-west corner within the extents, minus one row /
+  // column), scanned in pixel order; a pixel's 4 corners are 4 different cells,
+  // so at most one matches
+  const bool act = slice < NS;
+  if (t < HW) {
+    const int qy = t / W, qx = t - (t / W) * W;
+    const bool any = ext[0] <= ext[1];  // some pixel lands on the image (else no sources)
+    const int y0 = any ? max(0, qy - 1 - ext[3]) : 1, y1 = any ? min(H - 1, qy - ext[2]) : 0;
+    const int x0 = any ? max(0, qx - 1 - ext[1]) : 1, x1 = any ? min(W - 1, qx - ext[0]) : 0;
+    int n = 0;
+    for (int y = y0; y <= y1; ++y)
+      for (int xx = x0; xx <= x1; ++xx) {
+        const int p = y * W + xx;
+        const int4 o = tof[p];
+        const int k = o.x == t ? 0 : o.y == t ? 1 : o.z == t ? 2 : o.w == t ? 3 : -1;
+        if (k >= 0) {
+          if (n < kSmallM) {
+            const float4 w = twt[p];
+            lsp[n][t] = (unsigned short)p;
+            lsw[n][t] = k == 0 ? w.x : k == 1 ? w.y : k == 2 ? w.z : w.w;
+          }
+          ++n;
+        }
+      }
+    lcnt[t] = n;
+    if (n > kSmallM) {  // crowded cell: the rest of its list in the pool, same order
+      const int beg = atomicAdd(&ltop, n - kSmallM);
+      lbeg[t] = beg;
+      int m = 0;
+      for (int y = y0; y <= y1; ++y)
+        for (int xx = x0; xx <= x1; ++xx) {
+          const int p = y * W + xx;
+          const int4 o = tof[p];
+          const int k = o.x == t ? 0 : o.y == t ? 1 : o.z == t ? 2 : o.w == t ? 3 : -1;
+          if (k >= 0) {
+            if (m >= kSmallM) pool[beg + m - kSmallM] = (unsigned short)(p * 4 + k);
+            ++m;
+          }
+        }
+    }
+  }
+  __syncthreads();
+  if (!act) return;
+  const int n = lcnt[pp];
+  int sp[kSmallM];
+  float sw[kSmallM];
+#pragma unroll
+  for (int j = 0; j < kSmallM; ++j) {
+    sp[j] = j < n ? lsp[j][pp] : 0;
+    sw[j] = j < n ? lsw[j][pp] : 0.f;
+  }
+  const int pb = n > kSmallM ? lbeg[pp] : 0;
+  for (int c = slice; c < kSmallCG && c0 + c < C; c += NS) {
+    const float* gs = gst[c];
+    float acc = 0.f;
+#pragma unroll
+    for (int j = 0; j < kSmallM; ++j)
+      if (j < n) acc += gs[sp[j]] * sw[j];
+    for (int j = kSmallM; j < n; ++j) {  // crowded cell: the rest of its list from the pool
+      const int e = pool[pb + j - kSmallM], p = e >> 2, k = e & 3;
+      const float4 w = twt[p];
+      acc += gs[p] * (k == 0 ? w.x : k == 1 ? w.y : k == 2 ? w.z : w.w);
+    }
+    gx[((size_t)b * C + c0 + c) * HW + pp] = acc;
+  }
+}
+
 template <bool BORDER>
 void bwd_launch_pad(const float* x, const float* flow, long long fbs, const float* gout,
                     float* gx, float* gflow, int B, int C, int H, int W, hipStream_t s,
@@ -1138,6 +1351,15 @@ void bwd_launch_pad(const float* x, const float* flow, long long fbs, const floa
   // usf_set_variant(2, 2 / 3): lane-merged scatter with CS forced to 4 / 1
   // (whole-wave pixel runs) instead of the occupancy-driven choice
   const int v = variant_override(2);
+  // small images (decoder level 1): one launch (usf_set_variant(2, 7) where
+  // it fits; off by default, see USF_WARP_SMALL)
+  if ((v == 7 || (v < 0 && USF_WARP_SMALL)) && H * W <= kSmallMaxHW && H >= 2 && W >= 2 && (gx || gflow)) {
+    const int ngx = gx ? B * ((C + kSmallCG - 1) / kSmallCG) : 0;
+    const int ngf = gflow ? B * ((H * W + kSmallGFP - 1) / kSmallGFP) : 0;
+    hipLaunchKernelGGL((warp_bwd_small_kernel<BORDER>), dim3((unsigned)(ngx + ngf)), dim3(kSmallNT), 0, s, x, flow,
+                       fbs, gout, gx, gflow, B, C, H, W, ngx);
+    return;
+  }
   // binned gather (default with a workspace; usf_set_variant(2, 6) requires one)
   // (bin entries pack (py, px) into 16-bit halves)
   if (gx && ws && ws_bytes >= bin_layout(B, H, W).total && (v < 0 || v == 6) && H < 32768 && W < 65536) {
