@@ -8,8 +8,9 @@ into its channel slice of the concat buffer (usf_corr_fwd_ex_f32: output batch
 stride + activation epilogue), so the 81-channel cost map is neither written
 twice (activation pass) nor copied (cat). Backward reads its gradient from the
 concat gradient's slice (batch stride) and applies the LeakyReLU derivative:
-from the sign mask the forward wrote (its epilogue, or at the small levels
-whose forward splits its channel loop, its reduce), inside the backward
+from the sign mask the forward wrote (the tiled kernel's epilogue; at the
+small levels the small-image kernel's, or the channel split's reduce where a
+row is too wide for it), inside the backward
 kernel's gradient loads (usf_corr_bwd_ex_f32) at every level; the extras'
 gradients are views.
 """
