@@ -1158,6 +1158,7 @@ constexpr int kSmallMaxHW = 256;
 #define USF_WARP_SMALL_CG 32
 #endif
 constexpr int kSmallCG = USF_WARP_SMALL_CG;  // channels per grad_x workgroup
+static_assert(kSmallCG % (kSmallNT / kSmallMaxHW) == 0, "whole channels per (cell, slice) thread");
 constexpr int kSmallM = 8;     // list entries a thread keeps in registers
 constexpr int kSmallPool = 4 * kSmallMaxHW;
 constexpr int kSmallLD = (kSmallCG * kSmallMaxHW + kSmallNT - 1) / kSmallNT;  // staged floats per thread
@@ -1329,18 +1330,30 @@ __global__ __launch_bounds__(kSmallNT) void warp_bwd_small_kernel(const float* _
     sw[j] = j < n ? lsw[j][pp] : 0.f;
   }
   const int pb = n > kSmallM ? lbeg[pp] : 0;
-  for (int c = slice; c < kSmallCG && c0 + c < C; c += NS) {
-    const float* gs = gst[c];
-    float acc = 0.f;
+  // entry-major: each source's weight and pixel are read once and its CPT
+  // channels' grad_out reads are independent (a crowded cell's pool entries
+  // no longer form one dependent LDS chain per channel); per channel the
+  // entries still add in list order
+  constexpr int CPT = kSmallCG / NS;
+  float acc[CPT];
 #pragma unroll
-    for (int j = 0; j < kSmallM; ++j)
-      if (j < n) acc += gs[sp[j]] * sw[j];
-    for (int j = kSmallM; j < n; ++j) {  // crowded cell: the rest of its list from the pool
-      const int e = pool[pb + j - kSmallM], p = e >> 2, k = e & 3;
-      const float4 w = twt[p];
-      acc += gs[p] * (k == 0 ? w.x : k == 1 ? w.y : k == 2 ? w.z : w.w);
-    }
-    gx[((size_t)b * C + c0 + c) * HW + pp] = acc;
+  for (int i = 0; i < CPT; ++i) acc[i] = 0.f;
+  auto add = [&](int p, float w) {
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) acc[i] += gst[slice + NS * i][p] * w;
+  };
+#pragma unroll
+  for (int j = 0; j < kSmallM; ++j)
+    if (j < n) add(sp[j], sw[j]);
+  for (int j = kSmallM; j < n; ++j) {  // crowded cell: the rest of its list from the pool
+    const int e = pool[pb + j - kSmallM], p = e >> 2, k = e & 3;
+    const float4 w = twt[p];
+    add(p, k == 0 ? w.x : k == 1 ? w.y : k == 2 ? w.z : w.w);
+  }
+#pragma unroll
+  for (int i = 0; i < CPT; ++i) {
+    const int c = slice + NS * i;
+    if (c0 + c < C) gx[((size_t)b * C + c0 + c) * HW + pp] = acc[i];
   }
 }
 
