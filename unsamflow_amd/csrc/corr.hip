@@ -603,9 +603,9 @@ hipError_t launch_fwd(const float* x1, const float* x2, float* out, int B, int C
 // of its x1 row and of the x2 row y + dy - d (with the column halo as
 // zeros) at once: one load round trip, one barrier. Thread t computes quad
 // t % Q (4 pixels of one row, all K dx) over the channel slice t / Q; the
-// slices are added through LDS in slice order (so the result is
-// deterministic), and the same workgroup applies the mean, the LeakyReLU
-// epilogue and writes the sign-mask words of its rows.
+// slices are added through LDS in a fixed order (four interleaved chains,
+// then pairwise: deterministic), and the same workgroup applies the mean, the
+// LeakyReLU epilogue and writes the sign-mask words of its row.
 // Staging is plain buffer loads + ds_write: W = 13, 26 rows are not 16-byte
 // aligned, and the dword LDS-DMA form moved 64 KB per workgroup at a few
 // bytes per clock (measured: L1 37 us with it vs 18.6 us for the split pair).
