@@ -19,6 +19,6 @@ if [ "${PROF:-1}" = "1" ]; then
   export USF_ROCTX=1
   timeout -k 10 600 rocprofv3 --kernel-trace --stats --kernel-rename --marker-trace --output-format csv -d "$R/gpurun_out/prof" -o run -- python3 "$R/bench.py" --steps 10 --warmup 5 --no-cpu-baseline --no-replay > gpurun_out/bench_prof.json 2> gpurun_out/bench_prof.err || { echo "rocprof failed rc=$?"; tail -20 gpurun_out/bench_prof.err; exit 1; }
   unset USF_ROCTX
-  python tools/roofline_check.py gpurun_out/bench_prof.json gpurun_out/prof/run_kernel_stats.csv > gpurun_out/roofline_check.json || exit 1
+  python tools/roofline_check.py gpurun_out/bench_prof.json gpurun_out/prof/run_kernel_stats.csv gpurun_out/bench.json > gpurun_out/roofline_check.json || exit 1
 fi
 echo ALLDONE

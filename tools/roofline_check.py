@@ -10,7 +10,13 @@ also counts the warm-up steps; a site whose launch runs two kernels -- the
 split forward's reduce, the leaky backward's derivative pass, the photometric
 final reduction -- is the sum of both).
 
-Usage: python tools/roofline_check.py bench_prof.json run_kernel_stats.csv
+The profiler inflates the in-step time of two-kernel sites (the gap between
+their kernels), so the profiled run's own largest site can differ from the
+unprofiled bench's. With a third argument (the unprofiled bench.py line) the
+check is made for THAT run's roofline site and also reports its unprofiled
+in-step mean.
+
+Usage: python tools/roofline_check.py bench_prof.json run_kernel_stats.csv [bench.json]
 """
 import csv
 import json
@@ -37,10 +43,17 @@ def main():
         if st:
             entry["rel_diff"] = round(entry["rocprof_avg_us"] / row["in_step_us"] - 1, 4)
         sites.append(entry)
+    out = {}
+    if len(sys.argv) > 3:  # the unprofiled run's roofline site and mean
+        main_roof = json.loads(open(sys.argv[3]).read().strip().splitlines()[-1])["roofline"]
+        out["profiled_run_roofline_site"] = roof["site"]
+        roof = main_roof
     top = next(e for e in sites if e["site"] == roof["site"])
-    print(json.dumps({"roofline_site": roof["site"], "roofline_mean_us": roof["mean_us"],
-                      "rocprof_avg_us": top["rocprof_avg_us"], "rel_diff": top.get("rel_diff"),
-                      "sites": sites}, indent=1))
+    out = {"roofline_site": roof["site"], "roofline_mean_us": roof["mean_us"],
+           "rocprof_avg_us": top["rocprof_avg_us"],
+           "rel_diff": round(top["rocprof_avg_us"] / roof["mean_us"] - 1, 4) if top["rocprof_avg_us"] else None,
+           **out, "sites": sites}
+    print(json.dumps(out, indent=1))
     return 0 if top["rocprof_avg_us"] is not None else 1
 
 
