@@ -134,7 +134,8 @@ def test_variant_override_bounds(lib):
     assert n_fwd > 1 and n_bwd > 1
     assert lib.usf_set_variant(0, n_fwd) == -1 and b"bad op" in lib.usf_last_error_string()
     assert lib.usf_set_variant(4, 0) == -1
-    assert lib.usf_set_variant(3, 1) == 3 and lib.usf_set_variant(3, -1) == 3  # photometric: pair / tile / strip
+    assert lib.usf_set_variant(3, 0) == 1 and lib.usf_set_variant(3, -1) == 1  # photometric: the pair kernel only
+    assert lib.usf_set_variant(3, 1) == -1
     assert lib.usf_set_variant(2, 1) == 8 and lib.usf_set_variant(2, -1) == 8  # warp grad_x: 7 = small image
     assert lib.usf_set_variant(1, n_bwd - 1) == n_bwd
     assert lib.usf_set_variant(1, -1) == n_bwd

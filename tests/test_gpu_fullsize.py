@@ -106,3 +106,45 @@ def test_train_step_full_kitti_b1_vs_oracle(hip_device):
         ga = float(pc.grad.double().abs().sum())
         assert abs(float(pg.grad.double().sum()) - float(pc.grad.double().sum())) <= 2e-3 * ga + 1e-8, n
         assert abs(float(pg.grad.double().abs().sum()) - ga) <= 2e-3 * ga + 1e-8, n
+
+
+def test_train_step_full_sintel_mf_b1_vs_oracle(hip_device):
+    """SURVEY config 5 per GPU at its real size: Sintel 1024x448, the mask-feature
+    branch on (configs/sintel_aug+hg+mf.json:3-6: add_mask_corr, aggregation
+    "concat"; pwclite.py:317-361), B=1, K=32 piecewise-constant SAM segments --
+    the HIP step against the CPU oracle step (loss, flows, gradient sums), with
+    the same tolerances as the KITTI step above."""
+    from oracle.hashrng import hash_init_, uniform
+    from oracle.torch_ref import OracleCorrelation, oracle_occu_mask_backward
+    from unsamflow_amd.config import sintel_mf
+    from unsamflow_amd.harness import TrainStep, synthetic_pair
+
+    torch.set_num_threads(max(1, min(16, torch.get_num_threads())))
+    cfg = sintel_mf()
+    assert cfg.model.add_mask_corr
+    gpu = TrainStep(cfg, hip_device)
+    cpu = TrainStep(cfg, "cpu", corr_module=OracleCorrelation(4), warp_fn=oracle_flow_warp,
+                    occ_backward_fn=oracle_occu_mask_backward)
+    hash_init_(gpu.module, seed=3)
+    hash_init_(cpu.module, seed=3)
+    H, W = 448, 1024
+    im1 = torch.from_numpy(uniform((1, 3, H, W), 31))
+    im2 = torch.from_numpy(uniform((1, 3, H, W), 32))
+    _, _, s1, s2 = synthetic_pair(1, H, W, "cpu", seed=33, with_seg=True, n_seg=32)
+    d = hip_device
+    lg, fg = gpu.forward_loss(im1.to(d), im2.to(d), s1.to(d), s2.to(d))
+    lc, fc = cpu.forward_loss(im1, im2, s1, s2)
+    lg.backward()
+    lc.backward()
+    torch.cuda.synchronize(d)
+    assert abs(lg.item() - lc.item()) <= 1e-4 * abs(lc.item()) + 1e-6, (lg.item(), lc.item())
+    assert len(fg) == len(fc) == 5
+    for a, b in zip(fg, fc):
+        np.testing.assert_allclose(a.detach().cpu().numpy(), b.detach().numpy(), atol=1e-4, rtol=1e-3)
+    n_mask = 0
+    for (n, pg), pc in zip(gpu.module.named_parameters(), cpu.module.parameters()):
+        n_mask += "mask" in n
+        ga = float(pc.grad.double().abs().sum())
+        assert abs(float(pg.grad.double().sum()) - float(pc.grad.double().sum())) <= 2e-3 * ga + 1e-8, n
+        assert abs(float(pg.grad.double().abs().sum()) - ga) <= 2e-3 * ga + 1e-8, n
+    assert n_mask > 0  # the mask-feature branch's own parameters took part

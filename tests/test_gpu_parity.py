@@ -424,7 +424,7 @@ def test_occlusion_vs_oracle_full_size(hip_device, shape, scale):
 def test_corr_fwd_small_and_split_vs_tiled_and_oracle(hip_device, shape, split):
     """Small levels: the small-image kernel (one workgroup per sample, dy and
     row block, all channels staged at once; usf_corr_fwd_workspace == 0) or,
-    where its rows do not fit 64 KB of LDS, the channel split with its reduce
+    where its rows do not fit the 32 KB stage, the channel split with its reduce
     (workspace > 0). Either matches the tiled kernel (variant 4, <4,4,8,3,8>)
     and the fp64 oracle; with the LeakyReLU epilogue into a concat slice it
     matches the composition, and its sign mask equals the tiled kernel's."""
@@ -597,3 +597,36 @@ def test_warp_backward_small_image_flow_slice(hip_device):
     rx, rf = warp_backward_np(x, np.ascontiguousarray(f4[:, 2:]), g, "border")
     np.testing.assert_allclose(_np(gx), rx, atol=1e-4, rtol=1e-5)
     np.testing.assert_allclose(_np(gf), rf, atol=1e-4, rtol=1e-5)
+
+
+@pytest.mark.parametrize("d", [1, 2, 3])
+@pytest.mark.parametrize("shape", [(4, 64, 4, 13), (3, 48, 6, 26), (2, 40, 5, 10)])
+def test_corr_fwd_small_kernel_every_d_vs_oracle(hip_device, d, shape):
+    """fwd_plan sends the small levels to the small-image kernel for every d in
+    1..4; its staging (V = 1 / 2 column pairs, HALO = 4 or 8, the window
+    offsets) differs with d and with W's parity (advisor r03). Forward, the
+    LeakyReLU epilogue and its sign mask against the fp64 oracle."""
+    from unsamflow_amd import _lib, ops
+
+    B, C, H, W = shape
+    K = 2 * d + 1
+    lib = _lib.load()
+    assert lib.usf_corr_fwd_workspace(B, C, H, W, d) == 0  # the small kernel, not the split
+    x1 = hashrng.normal(shape, 70 + d)
+    x2 = hashrng.normal(shape, 80 + d)
+    t1, t2 = _dev(x1, hip_device), _dev(x2, hip_device)
+    ref = corr_forward_np(x1, x2, d)
+    np.testing.assert_allclose(_np(ops.corr_forward(t1, t2, d)), ref, atol=CORR_ATOL, rtol=CORR_RTOL)
+    cat = torch.full((B, K * K + 2, H, W), 7.0, device=hip_device)
+    mask = ops.corr_act_mask(B, H, W, d, hip_device)
+    ops.corr_forward_ex(t1, t2, d, cat[:, 1:1 + K * K], leaky_slope=0.1, act_mask=mask)
+    act = np.where(ref > 0, ref, ref * np.float32(0.1))
+    np.testing.assert_allclose(_np(cat[:, 1:1 + K * K]), act, atol=CORR_ATOL, rtol=CORR_RTOL)
+    assert float(cat[:, 0].min()) == 7.0 and float(cat[:, -1].max()) == 7.0
+    if mask is not None:
+        pos = (cat[:, 1:1 + K * K] > 0).reshape(B, K, K, H, W).cpu().numpy()
+        bits = np.zeros((B, K, H, (W + 3) // 4), np.uint64)
+        for dx in range(K):
+            for x in range(W):
+                bits[..., x // 4] |= pos[:, :, dx, :, x].astype(np.uint64) << np.uint64(4 * dx + x % 4)
+        assert np.array_equal(mask.cpu().numpy().view(np.uint64), bits)

@@ -30,6 +30,7 @@ CASES = [
     (1, 3, 3, 5, 1.0, "rand", "border"),
     (2, 3, 33, 47, 3.0, "rand", "zeros"),
     (2, 1, 20, 36, 2.0, "rand", "border"),
+    (2, 2, 21, 70, 2.0, "rand", "border"),  # the C == 2 instantiation (advisor r03)
     (8, 3, 64, 208, 4.0, "rand", "border"),
 ]
 
@@ -93,6 +94,7 @@ PAIR_CASES = [
     (2, 3, 24, 40, 2.0, "border"),
     (1, 3, 3, 5, 1.0, "border"),
     (2, 1, 33, 47, 3.0, "zeros"),
+    (2, 2, 19, 130, 2.0, "zeros"),
     (8, 3, 64, 208, 4.0, "border"),
 ]
 

@@ -686,9 +686,6 @@ __global__ __launch_bounds__(256) void corr_fwd_small_kernel(const float* __rest
   const int HW = H * W;
   const auto r1 = plane_buf(x1 + (size_t)b * C * HW, C * HW * 4);
   const auto r2 = plane_buf(x2 + (size_t)b * C * HW, C * HW * 4);
-#if defined(USF_SMALL_PROBE) && USF_SMALL_PROBE == 1
-  if (ep.slope == 12345.f)  // timing probe only: no staging
-#endif
   if ((W & 1) == 0 && (D & 1) == 0) {  // 8-byte column pairs (x2's halo starts at -D)
     if (tid < NT / 2)
       small_stage<NT / 2, F::U / 2, 2>(r1, sm, C, S1, y, 0, H, W, tid);
@@ -708,9 +705,6 @@ __global__ __launch_bounds__(256) void corr_fwd_small_kernel(const float* __rest
   const int cs = (C + NS - 1) / NS;
   const int ns = (C + cs - 1) / cs;  // slices that own channels
   const int qd = tid % Q, s = tid / Q;
-#if defined(USF_SMALL_PROBE) && USF_SMALL_PROBE == 2
-  if (ep.slope != 12345.f) return;  // timing probe only: staging alone
-#endif
   float acc[K][4];
 #pragma unroll
   for (int dx = 0; dx < K; ++dx)
@@ -732,17 +726,6 @@ __global__ __launch_bounds__(256) void corr_fwd_small_kernel(const float* __rest
     }
   }
   __syncthreads();  // staging images free: slice partials [s][dx * 4 + i][Q]
-#if defined(USF_SMALL_PROBE) && USF_SMALL_PROBE == 3
-  if (ep.slope != 12345.f) {  // timing probe only: staging + compute (acc kept live)
-    float t = 0.f;
-#pragma unroll
-    for (int dx = 0; dx < K; ++dx)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) t += acc[dx][i];
-    if (t == 12345.f) out[tid] = t;
-    return;
-  }
-#endif
   float* red = sm;
   if (s < ns) {
 #pragma unroll
@@ -762,9 +745,6 @@ __global__ __launch_bounds__(256) void corr_fwd_small_kernel(const float* __rest
     // slices added in a fixed order: four interleaved chains, then (0+1)+(2+3)
     float t[4] = {0.f, 0.f, 0.f, 0.f};
     int s2 = 0;
-#if defined(USF_SMALL_PROBE) && USF_SMALL_PROBE == 4
-    if (ep.slope == 12345.f)  // timing probe only: no slice sums
-#endif
     for (; s2 + 4 <= ns; s2 += 4) {
 #pragma unroll
       for (int k = 0; k < 4; ++k) t[k] += red[(s2 + k) * ss + idx];
@@ -773,13 +753,13 @@ __global__ __launch_bounds__(256) void corr_fwd_small_kernel(const float* __rest
     const float sum = (t[0] + t[1]) + (t[2] + t[3]);
     const float m = pow2 ? sum * inv : sum / cf;
     const float v = leaky ? (m > 0.f ? m : m * ep.slope) : m;
-    red[idx] = v;  // for the sign mask (this thread is the only reader of idx)
+    // the sign mask tests the mean m > 0, as the tiled epilogue and the split
+    // reduce do (the same bit as leaky(m) > 0 for slope >= 0; this thread is
+    // the only reader of idx)
+    red[idx] = m;
     if (x < W) out[(size_t)b * ep.out_bstride + (size_t)(dy * K + dx) * HW + y * W + x] = v;
   }
   if (!(leaky && ep.mask)) return;
-#if defined(USF_SMALL_PROBE) && USF_SMALL_PROBE == 5
-  if (ep.slope != 12345.f) return;  // timing probe only: no sign mask
-#endif
   __syncthreads();
   if (tid < Q) {
     // all K * 4 reads issued at once (a per-element column test here made them
@@ -1423,7 +1403,7 @@ namespace {
 
 static int g_variant[4] = {-1, -1, -1, -1};
 int variant_override(int op) { return __atomic_load_n(&g_variant[op], __ATOMIC_RELAXED); }
-int variant_count(int op) { return op == 0 ? kFwdCandidates : op == 1 ? kBwdCandidates : op == 2 ? 8 : 3; }
+int variant_count(int op) { return op == 0 ? kFwdCandidates : op == 1 ? kBwdCandidates : op == 2 ? 8 : 1; }
 void set_variant_override(int op, int index) { __atomic_store_n(&g_variant[op], index, __ATOMIC_RELAXED); }
 
 hipError_t corr_fwd_launch(const float* x1, const float* x2, float* out, int B, int C, int H,

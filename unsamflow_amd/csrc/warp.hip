@@ -1163,6 +1163,11 @@ constexpr int kSmallM = 8;     // list entries a thread keeps in registers
 constexpr int kSmallPool = 4 * kSmallMaxHW;
 constexpr int kSmallLD = (kSmallCG * kSmallMaxHW + kSmallNT - 1) / kSmallNT;  // staged floats per thread
 constexpr int kSmallGFP = 64;  // pixels per grad_flow workgroup (x 16 channel slices)
+// Static LDS of warp_bwd_small_kernel (below): about 64 KiB at kSmallCG = 32,
+// which needs gfx950's 160 KiB per workgroup (64 KiB targets cannot build it).
+constexpr int kSmallLdsBytes = kSmallMaxHW * (16 + 16 + 4 + 4 + kSmallM * (2 + 4) + 4 * kSmallCG) +
+                               kSmallPool * 2 + 2 * kSmallNT * 4 + 4 * 5;
+static_assert(kSmallLdsBytes <= 160 * 1024, "warp_bwd_small_kernel: LDS beyond gfx950's 160 KiB per workgroup");
 
 template <bool BORDER>
 __global__ __launch_bounds__(kSmallNT) void warp_bwd_small_kernel(const float* __restrict__ x,
