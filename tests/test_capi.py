@@ -136,7 +136,7 @@ def test_variant_override_bounds(lib):
     assert lib.usf_set_variant(4, 0) == -1
     assert lib.usf_set_variant(3, 0) == 1 and lib.usf_set_variant(3, -1) == 1  # photometric: the pair kernel only
     assert lib.usf_set_variant(3, 1) == -1
-    assert lib.usf_set_variant(2, 1) == 9 and lib.usf_set_variant(2, -1) == 9  # warp grad_x: 7 = small image, 8 = tile
+    assert lib.usf_set_variant(2, 1) == 8 and lib.usf_set_variant(2, -1) == 8  # warp grad_x: 7 = small image
     assert lib.usf_set_variant(1, n_bwd - 1) == n_bwd
     assert lib.usf_set_variant(1, -1) == n_bwd
 

@@ -112,42 +112,3 @@ def test_production_backward_site_vs_oracle(hip_device, B, C, H, W):
     torch.testing.assert_close(gx1.cpu().double(), r1, atol=1e-5, rtol=1e-5)
     torch.testing.assert_close(gx2.cpu().double(), r2, atol=1e-5, rtol=1e-5)
 
-
-@pytest.mark.parametrize("variant", [4, 5])
-@pytest.mark.parametrize("B,C,H,W", [(16, 32, 64, 208), (3, 20, 13, 60), (2, 96, 16, 52), (1, 100, 9, 8)])
-def test_dpp_window_backward_vs_oracle(hip_device, variant, B, C, H, W):
-    """The DPP-window backward (usf_set_variant(1, 4 / 5): 16-lane rows of
-    quads, neighbours' quads through v_fmac_f32_dpp, 56-column tiles) at the
-    L4 site, ragged tiles and channel chunks, a channel-grouped level and a
-    tiny image: the decoder's call with the sign mask, and the plain
-    backward's single directions, against the fp64 oracle (atol = rtol =
-    1e-5); reruns are bit-identical."""
-    from oracle.corr import corr_backward_torch64
-    from unsamflow_amd import _lib, ops
-
-    lib = _lib.load()
-    x1 = torch.from_numpy(hashrng.normal((B, C, H, W), 411)).to(hip_device)
-    x2 = torch.from_numpy(hashrng.normal((B, C, H, W), 412)).to(hip_device)
-    buf = torch.zeros((B, 81 + 3, H, W), device=hip_device)
-    mask = ops.corr_act_mask(B, H, W, 4, hip_device, C=C)
-    ops.corr_forward_ex(x1, x2, 4, buf[:, :81], 0.1, act_mask=mask)
-    g = torch.from_numpy(hashrng.normal((B, 81 + 3, H, W), 413)).to(hip_device)
-    act = buf[:, :81].cpu()
-    g_eff = torch.where(act > 0, g[:, :81].cpu(), g[:, :81].cpu() * 0.1)
-    r1, r2 = corr_backward_torch64(x1.cpu(), x2.cpu(), g_eff, 4)
-    q1, q2 = corr_backward_torch64(x1.cpu(), x2.cpu(), g[:, :81].cpu(), 4)
-    lib.usf_set_variant(1, variant)
-    try:
-        gx1, gx2 = ops.corr_backward_ex(x1, x2, g[:, :81], 4, True, True, act_out=buf[:, :81], leaky_slope=0.1,
-                                        act_mask=mask)
-        hx1, hx2 = ops.corr_backward_ex(x1, x2, g[:, :81], 4, True, True, act_out=buf[:, :81], leaky_slope=0.1,
-                                        act_mask=mask)
-        p1, _ = ops.corr_backward(x1, x2, g[:, :81].contiguous(), 4, True, False)
-        _, p2 = ops.corr_backward(x1, x2, g[:, :81].contiguous(), 4, False, True)
-    finally:
-        lib.usf_set_variant(1, -1)
-    torch.testing.assert_close(gx1.cpu().double(), r1, atol=1e-5, rtol=1e-5)
-    torch.testing.assert_close(gx2.cpu().double(), r2, atol=1e-5, rtol=1e-5)
-    torch.testing.assert_close(p1.cpu().double(), q1, atol=1e-5, rtol=1e-5)
-    torch.testing.assert_close(p2.cpu().double(), q2, atol=1e-5, rtol=1e-5)
-    assert torch.equal(gx1, hx1) and torch.equal(gx2, hx2)

@@ -73,7 +73,9 @@ def main():
     if "fwd" in a.ops:
         todo += [("corr_fwd", (a.batch, C, H, W)) for C, H, W in KITTI]
         todo += [("corr_fwd", s) for s in SURVEY.values()]
-    if "bwd" in a.ops:
+    if "bwdk" in a.ops.split(","):  # plain backward (no LeakyReLU) at the decoder's shapes
+        todo += [("corr_bwd", (a.batch, C, H, W, True, True)) for C, H, W in KITTI]
+    if "bwd" in a.ops.split(","):
         todo += [("corr_bwd", (*s, True, True)) for s in SURVEY.values()]
     for op, key in todo:
         us = device_time_us(site_launcher(op, key, dev), reps=20, iters=10)

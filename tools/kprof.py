@@ -52,11 +52,15 @@ def main():
     b = torch.empty_like(a)
     for _ in range(n):
         b.copy_(a)
-    for op, key in selected_sites():
-        fn = site_launcher(op, key, dev)
-        for _ in range(n):
-            fn()
-        torch.cuda.synchronize()
+    # KPROF_BWD_VARIANTS="-1,4": every site once per correlation-backward variant (usf_set_variant(1, v))
+    for v in [int(t) for t in os.environ.get("KPROF_BWD_VARIANTS", "-1").split(",")]:
+        lib.usf_set_variant(1, v)
+        for op, key in selected_sites():
+            fn = site_launcher(op, key, dev)
+            for _ in range(n):
+                fn()
+            torch.cuda.synchronize()
+    lib.usf_set_variant(1, -1)
     print("kprof done")
 
 

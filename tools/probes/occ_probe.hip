@@ -2,7 +2,7 @@
 // resident per CU at once. Every wave stamps s_memrealtime at start, spins for
 // ~20 us, stamps again and records HW_ID/XCC_ID; the host computes the maximum
 // number of simultaneously resident workgroups per CU.
-// Usage: occ_probe  (sweeps workgroup sizes at 36 KB of LDS)
+// Usage: occ_probe  (sweeps workgroup sizes at 36 KB of LDS) | occ_probe T:LDS_BYTES ...
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -25,12 +25,21 @@ __global__ void spin(unsigned long long* tr, int lds_floats) {
   }
 }
 
-int main() {
+int main(int argc, char** argv) {
   const int nwg = 2048;
   unsigned long long* tr;
   hipMalloc(&tr, (size_t)nwg * 16 * 4 * 8);
-  for (int nt : {192, 256, 384, 512, 576, 640, 1024}) {
-    for (int lds : {0, 36 * 1024}) {
+  std::vector<std::pair<int, int>> cfgs;
+  for (int a = 1; a < argc; ++a) {
+    int t = 0, l = 0;
+    if (sscanf(argv[a], "%d:%d", &t, &l) == 2) cfgs.push_back({t, l});
+  }
+  if (cfgs.empty())
+    for (int nt : {192, 256, 384, 512, 576, 640, 1024})
+      for (int lds : {0, 36 * 1024}) cfgs.push_back({nt, lds});
+  hipFuncSetAttribute(reinterpret_cast<const void*>(&spin), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  for (auto [nt, lds] : cfgs) {
+    {
       hipMemset(tr, 0, (size_t)nwg * 16 * 4 * 8);
       hipLaunchKernelGGL(spin, dim3(nwg), dim3(nt), lds, 0, tr, lds / 4);
       hipDeviceSynchronize();

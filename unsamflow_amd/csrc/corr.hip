@@ -104,20 +104,23 @@ __device__ __forceinline__ rsrc_t plane_rsrc(const float* plane, bool valid, int
 // one and puts an s_waitcnt vmcnt(0) in front of every ds_read, serialising
 // the prefetch with the FMAs. Completion is awaited explicitly (dma_wait_all +
 // barrier at the end of each stage). M0 holds the LDS destination (an asm
-// input, so the compiler materialises it); the nop is the M0-write -> LDS-DMA
-// hazard wait the compiler emits for the builtin.
+// input, so the compiler materialises it). hipcc pads no hazard inside an asm
+// statement, so the string opens with s_nop 4: the descriptor SGPRs may come
+// straight from a VALU write (v_readfirstlane, or a v_readlane reloading a
+// spilled SGPR), which a VMEM read needs 5 wait states behind
+// (cdna_hip_programming.md 5.7 item 2); it also covers the M0 write.
 template <int V>
 __device__ __forceinline__ void dma(const rsrc_t& rsrc, float* dst, int voff) {
   static_assert(V == 1 || V == 4, "dword or dwordx4 LDS-DMA");
   // low 32 bits of a generic LDS pointer = the LDS byte address (no null check)
   const int m0 = __builtin_amdgcn_readfirstlane((int)(uint32_t)reinterpret_cast<uintptr_t>(dst));
   if constexpr (V == 4)
-    asm volatile("s_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds"
+    asm volatile("s_nop 4\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds"
                  :
                  : "{m0}"(m0), "v"(voff), "s"(rsrc)
                  : "memory");
   else
-    asm volatile("s_nop 0\n\tbuffer_load_dword %1, %2, 0 offen lds"
+    asm volatile("s_nop 4\n\tbuffer_load_dword %1, %2, 0 offen lds"
                  :
                  : "{m0}"(m0), "v"(voff), "s"(rsrc)
                  : "memory");
@@ -1280,11 +1283,6 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(USF_BWD
     corr_bwd_tile<D, PX, SEGX, NW, CC, V, false, AM>(sm, x2, g, gx1, tile, group, b, C, H, W, tiles_x, cg, ep);
   } else if constexpr (MODE == 2) {
     corr_bwd_tile<D, PX, SEGX, NW, CC, V, true, AM>(sm, x1, g, gx2, tile, group, b, C, H, W, tiles_x, cg, ep);
-  } else if constexpr (MODE == 4) {
-    // both directions of a (tile, group) in sequence: the gx2 half's g slice
-    // was fetched into this XCD's L2 moments before by the gx1 half
-    corr_bwd_tile<D, PX, SEGX, NW, CC, V, false, AM>(sm, x2, g, gx1, tile, group, b, C, H, W, tiles_x, cg, ep);
-    corr_bwd_tile<D, PX, SEGX, NW, CC, V, true, AM>(sm, x1, g, gx2, tile, group, b, C, H, W, tiles_x, cg, ep);
   } else {
     if (b >= B)
       corr_bwd_tile<D, PX, SEGX, NW, CC, V, true, AM>(sm, x1, g, gx2, tile, group, b - B, C, H, W,
@@ -1307,7 +1305,7 @@ template <int D, int PX, int SEGX, int NW, int CC, int V, int MODE>
 hipError_t launch_bwd_mode(const float* x1, const float* x2, const float* g, float* gx1,
                            float* gx2, int B, int C, int H, int W, hipStream_t s, BwdEpi ep) {
   using F = BwdCfg<D, PX, SEGX, NW, CC, V>;
-  const int dirs = MODE == 3 ? 2 : 1;  // MODE 4: both directions inside each workgroup
+  const int dirs = MODE == 3 ? 2 : 1;
   const int tiles_x = (W + F::TW - 1) / F::TW;
   const int tiles_y = (H + F::TH - 1) / F::TH;
   const long units = (long)tiles_x * tiles_y * B * dirs;
@@ -1331,11 +1329,6 @@ hipError_t launch_bwd_mode(const float* x1, const float* x2, const float* g, flo
 template <int D, int PX, int SEGX, int NW, int CC, int V>
 hipError_t launch_bwd_v(const float* x1, const float* x2, const float* g, float* gx1, float* gx2,
                         int B, int C, int H, int W, hipStream_t s, BwdEpi ep) {
-#ifndef USF_BWD_SEQDIR
-#define USF_BWD_SEQDIR 0  // 1: one workgroup runs a tile's gx1 then its gx2 (MODE 4)
-#endif
-  if (gx1 && gx2 && USF_BWD_SEQDIR)
-    return launch_bwd_mode<D, PX, SEGX, NW, CC, V, 4>(x1, x2, g, gx1, gx2, B, C, H, W, s, ep);
   if (gx1 && gx2)
     return launch_bwd_mode<D, PX, SEGX, NW, CC, V, 3>(x1, x2, g, gx1, gx2, B, C, H, W, s, ep);
   hipError_t e = hipSuccess;
@@ -1355,196 +1348,6 @@ hipError_t launch_bwd(const float* x1, const float* x2, const float* g, float* g
   return launch_bwd_v<D, PX, SEGX, NW, CC, 1>(x1, x2, g, gx1, gx2, B, C, H, W, s, ep);
 }
 
-// ------------------------------------------------ backward, DPP window form --
-// The same gather formulas as corr_bwd_kernel (gx1 from g and x2, gx2 from the
-// shifted g and x1; one launch for both directions), with a lane layout built
-// for the x window instead of the column-major tile: a wave is 4 image rows x
-// 16 column quads, one 16-lane DPP row per image row, and each lane reads only
-// its OWN quad of a staged x row (one ds_read_b128). The 4-column halos either
-// side come from the neighbouring lanes through DPP (row_shr:1 / row_shl:1),
-// folded into the FMAs (v_fmac_f32_dpp): 20 of every 36 window FMAs read a
-// neighbour's register, the window costs a third of the LDS reads. The first
-// and last lane of each DPP row only provide their quad (their own sums see
-// a zero halo and are never stored), so a tile row owns 14 quads (56 columns)
-// and stages 64. A workgroup is 6 waves: 3 displacement-row groups (3 dy rows
-// of g in VGPRs each, as in corr_bwd_kernel) x 2 halves of an 8-row tile; the
-// three groups' partials are added through LDS in a fixed order (deterministic).
-constexpr int kDpTW = 56, kDpTH = 8, kDpNW = 6;  // owned tile, waves per workgroup
-constexpr int kDpRows = kDpTH + 8, kDpCols = 64;  // staged x region per channel (d = 4)
-
-// acc += src(lane - 1) * g  /  src(lane + 1) * g within the 16-lane row; the
-// row's first / last lane reads 0 (bound_ctrl): only the quad-owning lanes' sums are used
-__device__ __forceinline__ void fma_from_prev(float& acc, float src, float g) {
-  asm("v_fmac_f32_dpp %0, %1, %2 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "+v"(acc) : "v"(src), "v"(g));
-}
-__device__ __forceinline__ void fma_from_next(float& acc, float src, float g) {
-  asm("v_fmac_f32_dpp %0, %1, %2 row_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "+v"(acc) : "v"(src), "v"(g));
-}
-
-template <bool G2, bool AM, int CC>
-__device__ __forceinline__ void dpp_bwd_tile(float* sm, const float* __restrict__ xs, const float* __restrict__ g,
-                                             float* __restrict__ gx, int tile, int group, int b, int C, int H,
-                                             int W, int tiles_x, int cg, const BwdEpi& ep) {
-  constexpr int D = 4, K = 9, DYW = 3;
-  using X = StageImg<kDpRows, kDpCols, kDpCols, CC, 4, kDpNW>;
-  static_assert(X::PL == kDpRows * kDpCols, "whole DMA chunks per plane");
-  constexpr int XIMG = X::N;
-  float* red = sm + 2 * XIMG;  // [wave][CC][64 lanes][4]
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int dg = wave % 3, rh = wave / 3;  // displacement-row group, tile half
-  const int cbeg = group * cg, cend = min(C, cbeg + cg);
-  const int ty = tile / tiles_x, tx = tile - ty * tiles_x;
-  const int y0 = ty * kDpTH, x0 = tx * kDpTW;
-  const int rr = 4 * rh + (lane >> 4), q = lane & 15;  // tile row, quad of the DPP row
-  const int y = y0 + rr, xb = x0 - 4 + 4 * q;          // first column of the lane's quad
-  const bool owner = q >= 1 && q <= 14;
-  const int HW = H * W;
-
-  // g slice of this lane (quad-owning lanes only; the halo lanes' sums are unused)
-  float gv[DYW][K][4];
-  if (owner) {
-    bwd_load_g<D, 4, 8, 3, CC, 4, G2, AM, DYW, K>(gv, g + (size_t)b * ep.g_bstride, ep, b, dg, y, xb, H, W);
-  } else {
-#pragma unroll
-    for (int t = 0; t < DYW; ++t)
-#pragma unroll
-      for (int dx = 0; dx < K; ++dx)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) gv[t][dx][i] = 0.f;
-  }
-
-  X sx;
-  sx.init(wave, lane, y0 - D, x0 - 4, H, W);
-  const rsrc_t rx = plane_rsrc(xs + (size_t)b * C * HW, true, C * HW * 4);
-  const float cf = 1.f / (float)C, fc = (float)C;
-  const bool pow2 = (C & (C - 1)) == 0;
-  float* gxb = gx + (size_t)b * C * HW;
-  sx.load(rx, sm, wave, cbeg, cend, HW);
-  dma_wait_all();
-  __syncthreads();
-  int st = 0;
-  for (int c0 = cbeg; c0 < cend; c0 += CC, ++st) {
-    const float* cur = sm + (st & 1) * XIMG;
-    if (c0 + CC < cend) sx.load(rx, sm + ((st + 1) & 1) * XIMG, wave, c0 + CC, cend, HW);
-    float* rp = red + (wave * CC) * 256 + lane * 4;
-#pragma unroll 2
-    for (int c = 0; c < CC; ++c) {
-      float acc[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int t = 0; t < DYW; ++t) {
-        const int dy = dg * DYW + t;
-        const int row = rr + (G2 ? 2 * D - dy : dy);  // staged row of x
-        const float4 o4 = *reinterpret_cast<const float4*>(cur + c * X::PL + row * kDpCols + 4 * q);
-        const float own[4] = {o4.x, o4.y, o4.z, o4.w};
-#pragma unroll
-        for (int dx = 0; dx < K; ++dx) {
-          const int cs = G2 ? 2 * D - dx : dx;
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int j = i + cs;  // window element: 0-3 left quad, 4-7 own, 8-11 right quad
-            if (j < 4)
-              fma_from_prev(acc[i], own[j], gv[t][dx][i]);
-            else if (j < 8)
-              acc[i] = fmaf(gv[t][dx][i], own[j - 4], acc[i]);
-            else
-              fma_from_next(acc[i], own[j - 8], gv[t][dx][i]);
-          }
-        }
-      }
-      *reinterpret_cast<float4*>(rp + c * 256) = make_float4(acc[0], acc[1], acc[2], acc[3]);
-    }
-    dma_wait_all();
-    __syncthreads();  // partials complete; the next stage's image landed
-    // combine: item = (channel, tile half, lane); the three groups in order
-    const bool vec_out = (W & 3) == 0;
-    for (int o = tid; o < CC * 128; o += kDpNW * 64) {
-      const int c = o >> 7, slot = o & 127;
-      const int h = slot >> 6, l = slot & 63, ql = l & 15;
-      if (ql < 1 || ql > 14) continue;
-      const int yy = y0 + 4 * h + (l >> 4), xx = x0 - 4 + 4 * ql;
-      if (c0 + c >= cend || yy >= H || xx >= W) continue;
-      float4 sum = *reinterpret_cast<const float4*>(red + ((3 * h) * CC + c) * 256 + l * 4);
-#pragma unroll
-      for (int w2 = 1; w2 < 3; ++w2) {
-        const float4 v = *reinterpret_cast<const float4*>(red + ((3 * h + w2) * CC + c) * 256 + l * 4);
-        sum.x += v.x; sum.y += v.y; sum.z += v.z; sum.w += v.w;
-      }
-      if (pow2) {
-        sum.x *= cf; sum.y *= cf; sum.z *= cf; sum.w *= cf;
-      } else {
-        sum.x /= fc; sum.y /= fc; sum.z /= fc; sum.w /= fc;
-      }
-      float* o4 = gxb + (size_t)(c0 + c) * HW + yy * W + xx;
-      if (vec_out && xx + 3 < W) {
-        *reinterpret_cast<float4*>(o4) = sum;
-      } else {
-        if (xx < W) o4[0] = sum.x;
-        if (xx + 1 < W) o4[1] = sum.y;
-        if (xx + 2 < W) o4[2] = sum.z;
-        if (xx + 3 < W) o4[3] = sum.w;
-      }
-    }
-    __syncthreads();  // partial slots free for the next stage
-  }
-}
-
-template <int CC, int MODE, bool AM>
-__global__ __launch_bounds__(64 * kDpNW) __attribute__((amdgpu_waves_per_eu(3))) void corr_bwd_dpp_kernel(
-    const float* __restrict__ x1, const float* __restrict__ x2, const float* __restrict__ g,
-    float* __restrict__ gx1, float* __restrict__ gx2, int B, int C, int H, int W, int tiles_x, int cg,
-    BwdEpi ep) {
-  using X = StageImg<kDpRows, kDpCols, kDpCols, CC, 4, kDpNW>;
-  __shared__ __attribute__((aligned(16))) float sm[2 * X::N + kDpNW * CC * 256];
-  int w = linear_block();
-  if (USF_BWD_CHUNK > 0 && gridDim.x >= 16) w = xcd_chunk(w, gridDim.x * gridDim.y * gridDim.z, USF_BWD_CHUNK);
-  const int group = w % gridDim.y;
-  const int tile = (w / gridDim.y) % gridDim.x;
-  const int b = w / (gridDim.x * gridDim.y);
-  if constexpr (MODE == 1) {
-    dpp_bwd_tile<false, AM, CC>(sm, x2, g, gx1, tile, group, b, C, H, W, tiles_x, cg, ep);
-  } else if constexpr (MODE == 2) {
-    dpp_bwd_tile<true, AM, CC>(sm, x1, g, gx2, tile, group, b, C, H, W, tiles_x, cg, ep);
-  } else {
-    if (b >= B)
-      dpp_bwd_tile<true, AM, CC>(sm, x1, g, gx2, tile, group, b - B, C, H, W, tiles_x, cg, ep);
-    else
-      dpp_bwd_tile<false, AM, CC>(sm, x2, g, gx1, tile, group, b, C, H, W, tiles_x, cg, ep);
-  }
-}
-
-template <int CC, int MODE>
-hipError_t launch_bwd_dpp_mode(const float* x1, const float* x2, const float* g, float* gx1, float* gx2, int B,
-                               int C, int H, int W, hipStream_t s, BwdEpi ep) {
-  const int dirs = MODE == 3 ? 2 : 1;
-  const int tiles_x = (W + kDpTW - 1) / kDpTW, tiles_y = (H + kDpTH - 1) / kDpTH;
-  const long units = (long)tiles_x * tiles_y * B * dirs;
-  // ~2 resident workgroups per CU (512); every extra channel group re-reads g
-  int groups = (int)((512 + units - 1) / units);
-  groups = std::max(1, std::min(groups, (C + CC - 1) / CC));
-  const int cg = round_up((C + groups - 1) / groups, CC);
-  const dim3 grid(tiles_x * tiles_y, (C + cg - 1) / cg, B * dirs);
-  if (ep.mask)
-    hipLaunchKernelGGL((corr_bwd_dpp_kernel<CC, MODE, true>), grid, dim3(64 * kDpNW), 0, s, x1, x2, g, gx1, gx2, B, C,
-                       H, W, tiles_x, cg, ep);
-  else
-    hipLaunchKernelGGL((corr_bwd_dpp_kernel<CC, MODE, false>), grid, dim3(64 * kDpNW), 0, s, x1, x2, g, gx1, gx2, B,
-                       C, H, W, tiles_x, cg, ep);
-  return hipGetLastError();
-}
-
-// d = 4 and W % 4 == 0 only (16-byte staging and quads)
-template <int CC>
-hipError_t launch_bwd_dpp(const float* x1, const float* x2, const float* g, float* gx1, float* gx2, int B, int C,
-                          int H, int W, hipStream_t s, BwdEpi ep) {
-  if (W % 4 != 0) return hipErrorInvalidValue;
-  if (gx1 && gx2) return launch_bwd_dpp_mode<CC, 3>(x1, x2, g, gx1, gx2, B, C, H, W, s, ep);
-  hipError_t e = hipSuccess;
-  if (gx1) e = launch_bwd_dpp_mode<CC, 1>(x1, x2, g, gx1, gx2, B, C, H, W, s, ep);
-  if (e == hipSuccess && gx2) e = launch_bwd_dpp_mode<CC, 2>(x1, x2, g, gx1, gx2, B, C, H, W, s, ep);
-  return e;
-}
-
 hipError_t bwd_candidate_d4(int i, const float* x1, const float* x2, const float* g, float* gx1,
                             float* gx2, int B, int C, int H, int W, hipStream_t s, BwdEpi ep) {
   switch (i) {
@@ -1552,15 +1355,10 @@ hipError_t bwd_candidate_d4(int i, const float* x1, const float* x2, const float
     case 1: return launch_bwd<4, 4, 8, 3, 8>(x1, x2, g, gx1, gx2, B, C, H, W, s, ep);
     case 2: return launch_bwd<4, 4, 8, 9, 4>(x1, x2, g, gx1, gx2, B, C, H, W, s, ep);
     case 3: return launch_bwd<4, 4, 8, 9, 8>(x1, x2, g, gx1, gx2, B, C, H, W, s, ep);
-    // the DPP-window form needs 16-byte rows; other widths take the default
-    case 4: return W % 4 ? launch_bwd<4>(x1, x2, g, gx1, gx2, B, C, H, W, s, ep)
-                         : launch_bwd_dpp<4>(x1, x2, g, gx1, gx2, B, C, H, W, s, ep);
-    case 5: return W % 4 ? launch_bwd<4>(x1, x2, g, gx1, gx2, B, C, H, W, s, ep)
-                         : launch_bwd_dpp<6>(x1, x2, g, gx1, gx2, B, C, H, W, s, ep);
     default: return hipErrorInvalidValue;
   }
 }
-constexpr int kBwdCandidates = 6;
+constexpr int kBwdCandidates = 4;
 
 template <int D>
 hipError_t bwd_dispatch(const float* x1, const float* x2, const float* g, float* gx1, float* gx2,
@@ -1614,7 +1412,7 @@ namespace {
 
 static int g_variant[4] = {-1, -1, -1, -1};
 int variant_override(int op) { return __atomic_load_n(&g_variant[op], __ATOMIC_RELAXED); }
-int variant_count(int op) { return op == 0 ? kFwdCandidates : op == 1 ? kBwdCandidates : op == 2 ? 9 : 1; }
+int variant_count(int op) { return op == 0 ? kFwdCandidates : op == 1 ? kBwdCandidates : op == 2 ? 8 : 1; }
 void set_variant_override(int op, int index) { __atomic_store_n(&g_variant[op], index, __ATOMIC_RELAXED); }
 
 hipError_t corr_fwd_launch(const float* x1, const float* x2, float* out, int B, int C, int H,

@@ -1131,531 +1131,6 @@ void bwd_bins(const float* x, const float* flow, long long fbs, const float* gou
   hipLaunchKernelGGL((warp_gx_ovf_kernel<BORDER>), dim3(256), dim3(256), 0, s, flow, fbs, gout, ba, gx, C, H, W);
 }
 
-// ------------------------------------------------- one-pass tile backward --
-// grad_x (+ grad_flow) in one pass over a target tile, the default with a
-// caller workspace. A workgroup owns kTW x kTH target cells (and the same
-// pixels as grad_flow sources) for a group of channels; nothing but the
-// outlier list below goes through global memory between phases:
-//  1. taps: every source pixel within kTR of the tile (the region's middle
-//     columns) gets its tap (make_tap, the reference chain). A source is an
-//     INLIER when its north-west corner lies within [-kTR, kTR - 1] of it in
-//     both axes, so all four corners lie within kTR of the pixel; its packed
-//     corner cell and four weights go to LDS.
-//  2. lists: each target cell scans the (2 kTR + 1)^2 sources that can reach it
-//     in a fixed order and keeps the (source, weight) pairs whose corner is the
-//     cell -- deterministic, no atomics, no sort. Cells with more than kTL
-//     entries (strongly converging flow) make their wave rescan per channel.
-//  3. channels, kTCC at a time: grad_out and x over the region (the tile +
-//     kTR rows, + 4 columns either side: 16-byte aligned) are staged in LDS
-//     (the next chunk's loads in flight during this chunk's sums); each cell
-//     sums weight * grad_out over its list and writes gx once; each own pixel
-//     adds its grad_flow terms from the staged x corners (global loads for
-//     its outliers).
-//  4. outliers (the pixel's corner farther than kTR: large flow, border
-//     clamping) of the tile's own pixels go to a per-tile list, and
-//     warp_tile_ovf_kernel scatters them with float atomics after this kernel
-//     (in stream order, so after every gx store). With channel groups it also
-//     adds the groups' grad_flow partials in group order.
-// Traffic: grad_out and x are read (kTH + 2 kTR)(kTW + 8) / (kTW kTH) times
-// (in-image parts only; neighbouring tiles' halo rows mostly from L2), gx and
-// grad_flow written once, flow read ~1.3x: no cell metadata in HBM.
-#ifndef USF_WARP_TILE
-#define USF_WARP_TILE 0  // 1: the tile backward is the default grad_x path (else usf_set_variant(2, 8))
-#endif
-constexpr int kTW = 64, kTH = 16, kTNT = 512;  // 64 x 16 cells, 2 per thread (rows r, r + 8)
-constexpr int kTR = 2;                          // inlier radius
-constexpr int kTRW = kTW + 8;                   // region columns: x0 - 4 .. x0 + kTW + 3
-constexpr int kTRH = kTH + 2 * kTR;             // region rows: y0 - kTR .. y0 + kTH + kTR - 1
-constexpr int kTRN = kTRW * kTRH;               // region floats per plane
-constexpr int kTCW = kTW + 2 * kTR;             // candidate columns (region columns 2 .. kTW + 5)
-constexpr int kTCN = kTCW * kTRH;               // candidate sources
-constexpr int kTCC = 4;                         // channels per staged chunk
-constexpr int kTL = 8;                          // list entries a cell keeps in registers
-constexpr int kTQ = kTRN / 4;                   // region quads per plane
-constexpr int kTStageF = 2 * kTCC * kTRN;       // staged floats (grad_out and x planes)
-static_assert(kTQ <= kTNT && kTRN < 65536 && kTL % 2 == 0, "one region quad per thread and plane; 16-bit offsets");
-constexpr unsigned kTNoTap = 0xFFFFFFFFu;       // candidate with no inlier corner
-
-struct TileArgs {
-  int* ovf_cnt = nullptr;   // [B][ntiles] outliers listed per tile (written unconditionally)
-  int* ovf = nullptr;       // [B][ntiles][kTW * kTH] pixel index of each outlier
-  float* gfp = nullptr;     // [groups][B][2][HW] grad_flow partials (groups > 1)
-  int groups = 1, cg = 0, tiles_x = 0, ntiles = 0;
-};
-
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t tile_rsrc(const float* p, int bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), 0, bytes, 0x00020000);
-}
-__device__ __forceinline__ float4 tile_ld4(__amdgpu_buffer_rsrc_t r, int off) {
-  using u4 = unsigned int __attribute__((ext_vector_type(4)));
-  const u4 v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
-  return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
-}
-__device__ __forceinline__ float tile_ld1(__amdgpu_buffer_rsrc_t r, int off) {
-  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
-}
-constexpr int kTOff = 0x7FFFFFF0;  // past any plane's num_records: reads 0
-
-// One staged chunk: channels c0 .. c0 + kTCC - 1 of grad_out (and x) over the
-// region, quad q of each plane held by thread q (< kTQ). Branch-free: the
-// thread's in-plane byte offsets are fixed for the kernel (kTOff off the image),
-// the channel is the uniform soffset (clamped to the sample's end, so channels
-// past C read 0); a branch around a load made the compiler wait for every
-// earlier load at the merge (s_waitcnt vmcnt(0)) and serialised the prefetch.
-// V4 (W % 4 == 0): one 16-byte load per quad (a quad lies wholly on or off the
-// image); else four dword loads.
-struct TileStage {
-  float4 g[kTCC], x[kTCC];
-};
-struct TileOffs {
-  int v[4];  // V4: v[0] only
-};
-template <bool V4>
-__device__ __forceinline__ TileOffs tile_offsets(int t, int y0, int x0, int H, int W) {
-  const int qy = t / (kTRW / 4), qx = t - qy * (kTRW / 4);
-  const int gy = y0 - kTR + qy, gxx = x0 - 4 + 4 * qx;
-  const bool rowok = t < kTQ && (unsigned)gy < (unsigned)H;
-  TileOffs o;
-#pragma unroll
-  for (int e = 0; e < 4; ++e)
-    o.v[e] = rowok && (unsigned)(gxx + (V4 ? 0 : e)) < (unsigned)W ? 4 * (gy * W + gxx + (V4 ? 0 : e)) : kTOff;
-  return o;
-}
-__device__ __forceinline__ float4 tile_ld4s(__amdgpu_buffer_rsrc_t r, int off, int soff) {
-  using u4 = unsigned int __attribute__((ext_vector_type(4)));
-  const u4 v = __builtin_amdgcn_raw_buffer_load_b128(r, off, soff, 0);
-  return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
-}
-__device__ __forceinline__ float tile_ld1s(__amdgpu_buffer_rsrc_t r, int off, int soff) {
-  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, off, soff, 0));
-}
-template <bool WANT_GF, bool V4>
-__device__ __forceinline__ void tile_load(TileStage& st, __amdgpu_buffer_rsrc_t rg, __amdgpu_buffer_rsrc_t rx,
-                                          const TileOffs& o, int c0, int C, int HW) {
-  const int cap = C * HW * 4;  // num_records: a channel past C starts at the end (reads 0)
-#pragma unroll
-  for (int j = 0; j < kTCC; ++j) {
-    const int soff = __builtin_amdgcn_readfirstlane(min((c0 + j) * HW * 4, cap));
-    if constexpr (V4) {
-      st.g[j] = tile_ld4s(rg, o.v[0], soff);
-      if (WANT_GF) st.x[j] = tile_ld4s(rx, o.v[0], soff);
-    } else {
-      st.g[j] = make_float4(tile_ld1s(rg, o.v[0], soff), tile_ld1s(rg, o.v[1], soff), tile_ld1s(rg, o.v[2], soff),
-                            tile_ld1s(rg, o.v[3], soff));
-      if (WANT_GF)
-        st.x[j] = make_float4(tile_ld1s(rx, o.v[0], soff), tile_ld1s(rx, o.v[1], soff),
-                              tile_ld1s(rx, o.v[2], soff), tile_ld1s(rx, o.v[3], soff));
-    }
-  }
-}
-
-// compact tap of an own pixel for grad_flow: distances, clamp factors and the
-// north-west corner (offsets and masks are rebuilt from it where needed)
-struct OwnTap {
-  float s, n, w, e, mx, my;
-  int xw, yn;
-};
-
-template <bool BORDER, bool WANT_GF, bool V4>
-__global__ __launch_bounds__(kTNT) __attribute__((amdgpu_waves_per_eu(4))) void warp_tile_kernel(const float* __restrict__ x,
-                                                          const float* __restrict__ flow, long long fbs,
-                                                          const float* __restrict__ gout,
-                                                          float* __restrict__ gx, float* __restrict__ gflow,
-                                                          int C, int H, int W, TileArgs ta) {
-  __shared__ __attribute__((aligned(16))) float stage[kTStageF];  // [grad_out | x][kTCC][kTRN]
-  __shared__ __attribute__((aligned(16))) float4 tw[kTCN];         // candidate corner weights (nw, ne, sw, se)
-  __shared__ unsigned tkey[kTCN];                                   // candidate corner cell + masks, or kTNoTap
-  const int t = threadIdx.x;
-  const int tile = blockIdx.x, grp = blockIdx.y, b = blockIdx.z;
-  const int y0 = (tile / ta.tiles_x) * kTH, x0 = (tile % ta.tiles_x) * kTW;
-  const int c0g = grp * ta.cg, c1g = min(C, c0g + ta.cg);
-  const int HW = H * W;
-  const float* fb = flow + b * fbs;
-
-  // ---- 1. taps of the candidate sources (region rows 0 .. kTRH-1, columns 2 .. kTCW+1)
-  for (int i = t; i < kTCN; i += kTNT) {
-    const int ry = i / kTCW, rc = i - ry * kTCW;
-    const int py = y0 - kTR + ry, px = x0 - kTR + rc;
-    unsigned key = kTNoTap;
-    float4 w4 = make_float4(0.f, 0.f, 0.f, 0.f);
-    if ((unsigned)py < (unsigned)H && (unsigned)px < (unsigned)W) {
-      const int o = py * W + px;
-      const Tap tp = make_tap(fb[o], fb[HW + o], px, py, H, W, BORDER);
-      if (tp.fx >= (float)(px - kTR) && tp.fx <= (float)(px + kTR - 1) && tp.fy >= (float)(py - kTR) &&
-          tp.fy <= (float)(py + kTR - 1)) {
-        // north-west corner relative to the tile (+8 keeps both fields non-negative), corner masks
-        key = (unsigned)((tp.yn - y0 + 8) << 16 | (tp.xw - x0 + 8) << 4) |
-              (tp.m_nw ? 1u : 0u) | (tp.m_ne ? 2u : 0u) | (tp.m_sw ? 4u : 0u) | (tp.m_se ? 8u : 0u);
-        w4 = make_float4(tp.s * tp.e, tp.s * tp.w, tp.n * tp.e, tp.n * tp.w);
-      }
-    }
-    tkey[i] = key;
-    tw[i] = w4;
-  }
-  __syncthreads();
-
-  // ---- 2. per cell: its inlier sources, in scan order. A 25-bit mask of the
-  // candidates that hit the cell; its first kTL set bits become the list
-  // (static register slots). A wave with a longer list rescans per chunk.
-  const int cx = t % kTW, cy0 = t / kTW;  // cells (cy0, cx) and (cy0 + kTH / 2, cx)
-  constexpr int kTS = 2 * kTR + 1;        // scan window side
-  unsigned eoff[2][kTL / 2];  // two 16-bit region offsets per register
-  float ew[2][kTL];
-  unsigned hits_all[2];
-  bool crowded = false;
-  int nmax = 0;
-#pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    const int cy = cy0 + k * (kTH / 2);
-    unsigned hits = 0;
-#pragma unroll
-    for (int a = 0; a < kTS; ++a) {
-#pragma unroll
-      for (int bb = 0; bb < kTS; ++bb) {
-        const unsigned key = tkey[(cy + a) * kTCW + (cx + bb)];
-        const int dy = cy - ((int)(key >> 16) - 8), dx = cx - ((int)((key >> 4) & 0xFFF) - 8);
-        const bool hit = key != kTNoTap && (unsigned)dy < 2u && (unsigned)dx < 2u && ((key >> (2 * dy + dx)) & 1u);
-        hits |= hit ? 1u << (a * kTS + bb) : 0u;
-      }
-    }
-    hits_all[k] = hits;
-    const int n = __popc(hits);
-    crowded |= n > kTL;
-    nmax = max(nmax, min(n, kTL));
-#pragma unroll
-    for (int j = 0; j < kTL; ++j) {
-      const int bit = hits ? __ffs(hits) - 1 : 0;
-      const int a = bit / kTS, bb = bit - a * kTS;
-      const int i = (cy + a) * kTCW + (cx + bb);
-      const unsigned key = tkey[i];
-      const int corner = 2 * (cy - ((int)(key >> 16) - 8)) + (cx - ((int)((key >> 4) & 0xFFF) - 8));
-      const float4 w4 = tw[i];
-      const float w = corner == 0 ? w4.x : corner == 1 ? w4.y : corner == 2 ? w4.z : w4.w;
-      // the source in the staged region: row cy + a, column cx + bb + 2
-      const unsigned off = hits ? (unsigned)((cy + a) * kTRW + (cx + bb + 2)) : 0u;
-      if (j % 2 == 0)
-        eoff[k][j / 2] = off;
-      else
-        eoff[k][j / 2] |= off << 16;
-      ew[k][j] = hits ? w : 0.f;  // padding entries: weight 0 at offset 0
-      hits &= hits - 1;
-    }
-  }
-  // wave-uniform list length (shorter lists are padded with weight 0 at offset 0)
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) nmax = max(nmax, __shfl_xor(nmax, o));
-  const bool wave_crowded = __any(crowded);
-
-  // own pixels (= the cells): compact taps for grad_flow; an own pixel is an
-  // inlier exactly when its candidate entry got a key (the same tap)
-  OwnTap own[2];
-  bool own_in[2], own_inl[2];
-#pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    const int py = y0 + cy0 + k * (kTH / 2), px = x0 + cx;
-    own_in[k] = py < H && px < W;
-    own_inl[k] = tkey[(cy0 + k * (kTH / 2) + kTR) * kTCW + cx + kTR] != kTNoTap;
-    if (WANT_GF) {
-      const int o = own_in[k] ? py * W + px : 0;
-      const Tap tp = make_tap(fb[o], fb[HW + o], px, py, H, W, BORDER);
-      own[k] = OwnTap{tp.s, tp.n, tp.w, tp.e, tp.mx, tp.my, tp.xw, tp.yn};
-    }
-  }
-
-  // ---- 3. channel chunks
-  float* gs = stage;                  // [kTCC][kTRN] grad_out
-  float* xs = stage + kTCC * kTRN;    // [kTCC][kTRN] x
-  const auto rg = tile_rsrc(gout + (size_t)b * C * HW, C * HW * 4);
-  const auto rx = tile_rsrc(WANT_GF ? x + (size_t)b * C * HW : gout, C * HW * 4);
-  float dix[2] = {0.f, 0.f}, diy[2] = {0.f, 0.f};
-  TileStage st;
-  const TileOffs toff = tile_offsets<V4>(t, y0, x0, H, W);
-  tile_load<WANT_GF, V4>(st, rg, rx, toff, c0g, C, HW);
-  for (int c0 = c0g; c0 < c1g; c0 += kTCC) {
-    if (t < kTQ) {
-#pragma unroll
-      for (int j = 0; j < kTCC; ++j) {
-        reinterpret_cast<float4*>(gs + j * kTRN)[t] = st.g[j];
-        if (WANT_GF) reinterpret_cast<float4*>(xs + j * kTRN)[t] = st.x[j];
-      }
-    }
-    __syncthreads();
-    if (c0 + kTCC < c1g) tile_load<WANT_GF, V4>(st, rg, rx, toff, c0 + kTCC, C, HW);  // in flight meanwhile
-    const int nc = min(kTCC, c1g - c0);
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const int cy = cy0 + k * (kTH / 2);
-      float acc[kTCC];
-#pragma unroll
-      for (int j = 0; j < kTCC; ++j) acc[j] = 0.f;
-      if (!wave_crowded) {
-#pragma unroll
-        for (int e = 0; e < kTL; ++e) {
-          if (e < nmax) {
-#pragma unroll
-            for (int j = 0; j < kTCC; ++j)
-              acc[j] = fmaf(ew[k][e], gs[j * kTRN + ((eoff[k][e / 2] >> (16 * (e % 2))) & 0xFFFFu)], acc[j]);
-          }
-        }
-      } else {
-        // a cell of this wave has more than kTL sources: walk its whole hit mask (same order)
-        unsigned hits = hits_all[k];
-        while (__any(hits != 0u)) {
-          const int bit = hits ? __ffs(hits) - 1 : 0;
-          const int a = bit / kTS, bb = bit - a * kTS;
-          const int i = (cy + a) * kTCW + (cx + bb);
-          const unsigned key = tkey[i];
-          const int corner = 2 * (cy - ((int)(key >> 16) - 8)) + (cx - ((int)((key >> 4) & 0xFFF) - 8));
-          const float4 w4 = tw[i];
-          const float w = hits ? (corner == 0 ? w4.x : corner == 1 ? w4.y : corner == 2 ? w4.z : w4.w) : 0.f;
-          const int off = hits ? (cy + a) * kTRW + (cx + bb + 2) : 0;
-#pragma unroll
-          for (int j = 0; j < kTCC; ++j) acc[j] = fmaf(w, gs[j * kTRN + off], acc[j]);
-          hits &= hits - 1;
-        }
-      }
-      const int qy = y0 + cy, qx = x0 + cx;
-      if (own_in[k]) {
-        float* gq = gx + ((size_t)b * C + c0) * HW + qy * W + qx;
-#pragma unroll
-        for (int j = 0; j < kTCC; ++j)
-          if (j < nc) gq[(size_t)j * HW] = acc[j];
-      }
-      if (WANT_GF && own_in[k]) {
-        const OwnTap& tp = own[k];
-        if (own_inl[k]) {
-          // inlier: its corners lie in the staged region; staged zeros stand
-          // for the masked (off-image) corners
-          const int o = (tp.yn - (y0 - kTR)) * kTRW + (tp.xw - (x0 - 4));
-          const int og = (cy + kTR) * kTRW + cx + 4;
-#pragma unroll
-          for (int j = 0; j < kTCC; ++j) {
-            if (j >= nc) break;
-            const float* xc = xs + j * kTRN + o;
-            const float go = gs[j * kTRN + og];
-            const float vnw = xc[0], vne = xc[1], vsw = xc[kTRW], vse = xc[kTRW + 1];
-            dix[k] += ((vne - vnw) * tp.s + (vse - vsw) * tp.n) * go;
-            diy[k] += ((vsw - vnw) * tp.e + (vse - vne) * tp.w) * go;
-          }
-        } else {
-          // outlier: corners anywhere, read from global memory
-          const bool vxw = (unsigned)tp.xw < (unsigned)W, vxe = (unsigned)(tp.xw + 1) < (unsigned)W;
-          const bool vyn = (unsigned)tp.yn < (unsigned)H, vys = (unsigned)(tp.yn + 1) < (unsigned)H;
-          const int onw = tp.yn * W + tp.xw;
-          const int og = (cy + kTR) * kTRW + cx + 4;
-#pragma unroll
-          for (int j = 0; j < kTCC; ++j) {
-            if (j >= nc) break;
-            const float* xc = x + ((size_t)b * C + c0 + j) * HW;
-            const float go = gs[j * kTRN + og];
-            const float vnw = vxw && vyn ? xc[onw] : 0.f;
-            const float vne = vxe && vyn ? xc[onw + 1] : 0.f;
-            const float vsw = vxw && vys ? xc[onw + W] : 0.f;
-            const float vse = vxe && vys ? xc[onw + W + 1] : 0.f;
-            dix[k] += ((vne - vnw) * tp.s + (vse - vsw) * tp.n) * go;
-            diy[k] += ((vsw - vnw) * tp.e + (vse - vne) * tp.w) * go;
-          }
-        }
-      }
-    }
-    __syncthreads();  // the chunk's stages are read: the next chunk may overwrite them
-  }
-
-  // ---- 4. grad_flow (or this group's partial) and the tile's outliers
-  const size_t tslot = (size_t)b * ta.ntiles + tile;
-#pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    if (!own_in[k]) continue;
-    const int p = (y0 + cy0 + k * (kTH / 2)) * W + x0 + cx;
-    if (WANT_GF) {
-      const float ggx = dix[k] * own[k].mx, ggy = diy[k] * own[k].my;
-      if (ta.groups > 1) {  // this group's channel sums; the overflow kernel adds the groups in order
-        float* gf = ta.gfp + ((size_t)grp * gridDim.z + b) * 2 * HW + p;
-        gf[0] = ggx;
-        gf[HW] = ggy;
-      } else {
-        float* gf = gflow + (size_t)b * 2 * HW + p;
-        gf[0] = (ggx / (float)(W - 1)) * 2.0f;
-        gf[HW] = (ggy / (float)(H - 1)) * 2.0f;
-      }
-    }
-  }
-  // outliers with a corner on the image: listed once (group 0) for the
-  // scatter, in cell order (row k * kTH/2 + cy0, column cx) by a block-wide
-  // prefix count, so that runs of outliers sharing a cell (a border-clamped
-  // strip) are neighbours in the list and merge in the scatter's wave scan
-  bool lst[2];
-#pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    lst[k] = false;
-    if (grp == 0 && own_in[k] && !own_inl[k]) {
-      const int py = y0 + cy0 + k * (kTH / 2), px = x0 + cx;
-      const Tap tp = make_tap(fb[py * W + px], fb[HW + py * W + px], px, py, H, W, BORDER);
-      lst[k] = tp.m_nw || tp.m_ne || tp.m_sw || tp.m_se;
-    }
-  }
-  __shared__ int wcnt[2][kTNT / 64];
-  const int wv = t >> 6, ln = t & 63;
-  const unsigned long long below = ln == 0 ? 0ull : (~0ull >> (64 - ln));
-  unsigned long long bal[2];
-#pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    bal[k] = __ballot(lst[k]);
-    if (ln == 0) wcnt[k][wv] = __popcll(bal[k]);
-  }
-  __syncthreads();
-  int base = 0;  // entries before this lane's first cell: all of k = 0's rows come first
-#pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    int pre = 0, tot = 0;
-    for (int w2 = 0; w2 < kTNT / 64; ++w2) {
-      pre += w2 < wv ? wcnt[k][w2] : 0;
-      tot += wcnt[k][w2];
-    }
-    if (lst[k])
-      ta.ovf[tslot * (kTW * kTH) + base + pre + __popcll(bal[k] & below)] =
-          (y0 + cy0 + k * (kTH / 2)) * W + x0 + cx;
-    base += tot;
-  }
-  if (grp == 0 && t == 0) ta.ovf_cnt[tslot] = base;
-}
-
-// After warp_tile_kernel: the listed outliers of each tile scatter w * gout to
-// their four corners (float atomics; lanes = (entry, channel slice)), and with
-// channel groups every pixel's grad_flow is the sum of the groups' partials
-// (fixed group order), then norm_grid's scaling.
-template <bool BORDER>
-__global__ __launch_bounds__(256) void warp_tile_ovf_kernel(const float* __restrict__ flow, long long fbs,
-                                                            const float* __restrict__ gout, float* __restrict__ gx,
-                                                            float* __restrict__ gflow, int C, int H, int W,
-                                                            TileArgs ta) {
-  const int tile = blockIdx.x, b = blockIdx.y;
-  const int HW = H * W;
-  const size_t tslot = (size_t)b * ta.ntiles + tile;
-  const int t = threadIdx.x;
-  if (ta.groups > 1 && gflow) {
-    const int y0 = (tile / ta.tiles_x) * kTH, x0 = (tile % ta.tiles_x) * kTW;
-    for (int i = t; i < kTW * kTH; i += 256) {
-      const int py = y0 + i / kTW, px = x0 + i % kTW;
-      if (py >= H || px >= W) continue;
-      const int p = py * W + px;
-      float sx = 0.f, sy = 0.f;
-      for (int g = 0; g < ta.groups; ++g) {
-        const float* gp = ta.gfp + ((size_t)g * gridDim.y + b) * 2 * HW + p;
-        sx += gp[0];
-        sy += gp[HW];
-      }
-      gflow[(size_t)b * 2 * HW + p] = (sx / (float)(W - 1)) * 2.0f;
-      gflow[(size_t)b * 2 * HW + HW + p] = (sy / (float)(H - 1)) * 2.0f;
-    }
-  }
-  if (!gx) return;
-  const int n = ta.ovf_cnt[tslot];
-  if (n <= 0) return;
-  const int* list = ta.ovf + tslot * (kTW * kTH);
-  const float* fb = flow + b * fbs;
-  // a wave takes 64 consecutive list entries (lane = entry) x kOvfCh channels;
-  // runs of entries on the same north-west cell are summed by the segmented
-  // shuffle scan and only run tails issue atomics (as warp_gx_ovf_kernel)
-  const int lane = t & 63, wv = t >> 6;
-  const int ngrp = (C + kOvfCh - 1) / kOvfCh;
-  const int units = ((n + 63) / 64) * ngrp;
-  for (int u = wv; u < units; u += 4) {
-    const int chunk = u / ngrp, grpc = u - chunk * ngrp;
-    const int e = chunk * 64 + lane;
-    const bool valid = e < n;
-    const int p = valid ? list[e] : 0;
-    const int py = p / W, px = p - py * W;
-    Tap tp = make_tap(fb[p], fb[HW + p], px, py, H, W, BORDER);
-    if (!valid) tp.m_nw = tp.m_ne = tp.m_sw = tp.m_se = false;
-    const bool any = tp.m_nw || tp.m_ne || tp.m_sw || tp.m_se;
-    const int key = any ? (tp.yn + 1) * (W + 1) + tp.xw + 1 : -(lane + 2);
-    const int kl = __shfl_up(key, 1);
-    const bool head = lane == 0 || kl != key;
-    const unsigned long long heads = __ballot(head);
-    const unsigned long long upto = lane == 63 ? ~0ull : ((2ull << lane) - 1);
-    RowRuns r;
-    r.pos = lane - (63 - __clzll(heads & upto));
-    r.tail = lane == 63 || ((heads >> (lane + 1)) & 1ull) != 0;
-    int m = r.pos;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) m = max(m, __shfl_xor(m, o));
-    r.maxlen = m + 1;
-    const float wv4[4] = {tp.s * tp.e, tp.s * tp.w, tp.n * tp.e, tp.n * tp.w};
-    const bool mk[4] = {tp.m_nw, tp.m_ne, tp.m_sw, tp.m_se};
-    const int ok[4] = {tp.o_nw, tp.o_ne, tp.o_sw, tp.o_se};
-    const int c0 = grpc * kOvfCh;
-    float go[kOvfCh];
-#pragma unroll
-    for (int j = 0; j < kOvfCh; ++j) go[j] = valid && c0 + j < C ? gout[((size_t)b * C + c0 + j) * HW + p] : 0.f;
-#pragma unroll
-    for (int j = 0; j < kOvfCh; ++j) {
-      const size_t bs = ((size_t)b * C + c0 + j) * HW;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const float v = run_sum(go[j] * wv4[k], r);  // every lane takes part (shuffles)
-        if (r.tail && mk[k] && c0 + j < C) atomicAdd(gx + bs + ok[k], v);
-      }
-    }
-  }
-}
-
-// workspace of the tile backward (bytes), 0 if it does not apply
-struct TileLayout {
-  long long cnt_off, ovf_off, gfp_off, total;
-};
-inline TileLayout tile_layout(int B, int H, int W, int groups, bool want_gf) {
-  auto al = [](long long v) { return (v + 255) & ~255LL; };
-  const long long tiles = (long long)((W + kTW - 1) / kTW) * ((H + kTH - 1) / kTH);
-  TileLayout L;
-  L.cnt_off = 0;
-  L.ovf_off = al(4 * tiles * B);
-  L.gfp_off = al(L.ovf_off + 4LL * tiles * B * kTW * kTH);
-  L.total = al(L.gfp_off + (groups > 1 && want_gf ? 4LL * groups * B * 2 * H * W : 0));
-  return L;
-}
-// channel groups: about 2 workgroups per CU (512 on the chip) where the tiles
-// alone give fewer, at least kTCC channels per group
-inline int tile_groups(int B, int C, int H, int W) {
-  const long units = (long)B * ((W + kTW - 1) / kTW) * ((H + kTH - 1) / kTH);
-  int g = (int)std::max<long>(1, (512 + units - 1) / units);
-  g = std::min(g, std::max(1, C / kTCC));
-  return g;
-}
-
-template <bool BORDER>
-void bwd_tile(const float* x, const float* flow, long long fbs, const float* gout, float* gx, float* gflow, int B,
-              int C, int H, int W, void* ws, hipStream_t s) {
-  const int groups = tile_groups(B, C, H, W);
-  const TileLayout L = tile_layout(B, H, W, groups, gflow != nullptr);
-  char* w = static_cast<char*>(ws);
-  TileArgs ta;
-  ta.ovf_cnt = reinterpret_cast<int*>(w + L.cnt_off);
-  ta.ovf = reinterpret_cast<int*>(w + L.ovf_off);
-  ta.gfp = reinterpret_cast<float*>(w + L.gfp_off);
-  ta.groups = groups;
-  ta.cg = round_up((C + groups - 1) / groups, kTCC);
-  ta.groups = (C + ta.cg - 1) / ta.cg;
-  ta.tiles_x = (W + kTW - 1) / kTW;
-  ta.ntiles = ta.tiles_x * ((H + kTH - 1) / kTH);
-  const dim3 grid((unsigned)ta.ntiles, (unsigned)ta.groups, (unsigned)B);
-  const bool v4 = (W & 3) == 0;
-  if (gflow && v4)
-    hipLaunchKernelGGL((warp_tile_kernel<BORDER, true, true>), grid, dim3(kTNT), 0, s, x, flow, fbs, gout, gx, gflow,
-                       C, H, W, ta);
-  else if (gflow)
-    hipLaunchKernelGGL((warp_tile_kernel<BORDER, true, false>), grid, dim3(kTNT), 0, s, x, flow, fbs, gout, gx,
-                       gflow, C, H, W, ta);
-  else if (v4)
-    hipLaunchKernelGGL((warp_tile_kernel<BORDER, false, true>), grid, dim3(kTNT), 0, s, x, flow, fbs, gout, gx,
-                       gflow, C, H, W, ta);
-  else
-    hipLaunchKernelGGL((warp_tile_kernel<BORDER, false, false>), grid, dim3(kTNT), 0, s, x, flow, fbs, gout, gx,
-                       gflow, C, H, W, ta);
-  hipLaunchKernelGGL((warp_tile_ovf_kernel<BORDER>), dim3((unsigned)ta.ntiles, (unsigned)B), dim3(256), 0, s, flow,
-                     fbs, gout, gx, gflow, C, H, W, ta);
-}
-
 // --------------------------------------------------- small-image backward --
 // Decoder level 1 (batch 16 x 128 x 8 x 26: 208 pixels a sample): the binned
 // gather is four launches of a few workgroups each, ~20 us of latency chains.
@@ -1903,16 +1378,9 @@ void bwd_launch_pad(const float* x, const float* flow, long long fbs, const floa
                        fbs, gout, gx, gflow, B, C, H, W, ngx);
     return;
   }
-  // one-pass tile backward (default with a workspace; usf_set_variant(2, 8) requires one)
-  if (gx && ws && (v == 8 || (v < 0 && USF_WARP_TILE)) &&
-      ws_bytes >= tile_layout(B, H, W, tile_groups(B, C, H, W), gflow != nullptr).total) {
-    bwd_tile<BORDER>(x, flow, fbs, gout, gx, gflow, B, C, H, W, ws, s);
-    return;
-  }
-  // binned gather (the default with a workspace unless USF_WARP_TILE; usf_set_variant(2, 6))
+  // binned gather (default with a workspace; usf_set_variant(2, 6) requires one)
   // (bin entries pack (py, px) into 16-bit halves)
-  if (gx && ws && ws_bytes >= bin_layout(B, H, W).total && (v == 6 || (v < 0 && !USF_WARP_TILE)) && H < 32768 &&
-      W < 65536) {
+  if (gx && ws && ws_bytes >= bin_layout(B, H, W).total && (v < 0 || v == 6) && H < 32768 && W < 65536) {
     bwd_bins<BORDER>(x, flow, fbs, gout, gx, gflow, B, C, H, W, ws, s);
     return;
   }
@@ -2143,12 +1611,7 @@ hipError_t warp_bwd_launch(const float* x, const float* flow, long long fbs, con
   return hipGetLastError();
 }
 
-long long warp_bwd_workspace(int B, int H, int W) {
-  // the tile path's largest channel-group count for this shape (C >= 4 * groups)
-  const long units = (long)B * ((W + kTW - 1) / kTW) * ((H + kTH - 1) / kTH);
-  const int gmax = (int)std::max<long>(1, (512 + units - 1) / units);
-  return std::max(bin_layout(B, H, W).total, tile_layout(B, H, W, gmax, true).total);
-}
+long long warp_bwd_workspace(int B, int H, int W) { return bin_layout(B, H, W).total; }
 
 hipError_t splat_launch(const float* flow, long long fbs, float* map, int B, int H, int W,
                         bool absolute, hipStream_t s) {

@@ -12,7 +12,6 @@ struct Tap {
   bool m_nw, m_ne, m_sw, m_se;  // corner inside the image
   float n, s, w, e;             // distances (see header)
   float mx, my;                 // d(ix)/d(gx), d(iy)/d(gy) incl. clamp mask
-  float fx, fy;                 // floor(ix), floor(iy) as floats (range tests; NaN-safe)
 };
 
 __device__ __forceinline__ inline Tap make_tap(float u, float v, int x, int y, int H, int W,
@@ -42,8 +41,6 @@ __device__ __forceinline__ inline Tap make_tap(float u, float v, int x, int y, i
     else if (iy >= hm1) { iy = hm1; t.my = 0.f; }
   }
   const float fx = floorf(ix), fy = floorf(iy);
-  t.fx = fx;
-  t.fy = fy;
   t.w = ix - fx;
   t.e = 1.0f - t.w;
   t.n = iy - fy;
