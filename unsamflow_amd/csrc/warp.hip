@@ -55,6 +55,49 @@ __device__ __forceinline__ void warp_block(int& bx, int& b) {
   }
 }
 
+#ifndef USF_WARP_FWD_PAIR
+#define USF_WARP_FWD_PAIR 1  // forward L4 23.9 -> 13.1 us, L2 11.8 -> 7.5 us (profiles/ab_r04/warp_corner_pairs.json)
+#endif
+#ifndef USF_WARP_BWD_PAIR
+#define USF_WARP_BWD_PAIR 0
+#endif
+constexpr int kWarpOffNone = 0x7FFFFFF0;  // buffer offset past num_records: reads 0
+
+// A corner row's two taps are neighbours in memory, so each row is ONE 8-byte
+// load per channel (2 gathers per pixel and channel instead of 4: these
+// gathers are bound by address processing, not bytes). The pair starts at
+// lo = clamp(xw, 0, W - 2), so it never leaves the row where a corner is valid;
+// at xw = -1 / W - 1 the valid corner is the pair's other half (swp). A row off
+// the image gets an offset past num_records (reads 0; adding a channel base
+// keeps it past). Needs W >= 2. Values of masked corners are zeroed, as before.
+struct PairTap {
+  unsigned on, os;  // byte offsets of the north / south pairs in a channel plane
+  bool swp;
+};
+__device__ __forceinline__ PairTap pair_tap(const Tap& tp, int W) {
+  PairTap q;
+  const int lo = min(max(tp.xw, 0), W - 2);
+  q.swp = tp.xw != lo;
+  q.on = tp.m_nw || tp.m_ne ? 4u * (unsigned)(tp.yn * W + lo) : (unsigned)kWarpOffNone;
+  q.os = tp.m_sw || tp.m_se ? 4u * (unsigned)((tp.yn + 1) * W + lo) : (unsigned)kWarpOffNone;
+  return q;
+}
+__device__ __forceinline__ void pair_corners(__amdgpu_buffer_rsrc_t rs, const PairTap& q, const Tap& tp, unsigned cb,
+                                             float& vnw, float& vne, float& vsw, float& vse) {
+  using u32x2 = unsigned int __attribute__((ext_vector_type(2)));
+  const u32x2 pn = __builtin_amdgcn_raw_buffer_load_b64(rs, (int)(q.on + cb), 0, 0);
+  const u32x2 ps = __builtin_amdgcn_raw_buffer_load_b64(rs, (int)(q.os + cb), 0, 0);
+  const float n0 = __uint_as_float(pn.x), n1 = __uint_as_float(pn.y);
+  const float s0 = __uint_as_float(ps.x), s1 = __uint_as_float(ps.y);
+  vnw = tp.m_nw ? (q.swp ? n1 : n0) : 0.f;
+  vne = tp.m_ne ? (q.swp ? n0 : n1) : 0.f;
+  vsw = tp.m_sw ? (q.swp ? s1 : s0) : 0.f;
+  vse = tp.m_se ? (q.swp ? s0 : s1) : 0.f;
+}
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t sample_rsrc(const float* p, int bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), 0, bytes, 0x00020000);
+}
+
 template <bool BORDER, int CS>
 __global__ __launch_bounds__(256) void warp_fwd_kernel(const float* __restrict__ x,
                                                        const float* __restrict__ flow,
@@ -72,8 +115,19 @@ __global__ __launch_bounds__(256) void warp_fwd_kernel(const float* __restrict__
   const float* fb = flow + b * fbs;
   const Tap tp = make_tap(fb[p], fb[HW + p], xx, y, H, W, BORDER);
   const float wnw = tp.s * tp.e, wne = tp.s * tp.w, wsw = tp.n * tp.e, wse = tp.n * tp.w;
-  const float* xb = x + (size_t)b * C * HW;
   float* ob = out + (size_t)b * C * HW + p;
+  if (USF_WARP_FWD_PAIR && W >= 2) {  // corner pairs (pair_tap)
+    const PairTap q = pair_tap(tp, W);
+    const auto rs = sample_rsrc(x + (size_t)b * C * HW, 4 * C * HW);
+#pragma unroll 4
+    for (int c = slice; c < C; c += CS) {
+      float vnw, vne, vsw, vse;
+      pair_corners(rs, q, tp, 4u * (unsigned)(c * HW), vnw, vne, vsw, vse);
+      ob[(size_t)c * HW] = vnw * wnw + vne * wne + vsw * wsw + vse * wse;
+    }
+    return;
+  }
+  const float* xb = x + (size_t)b * C * HW;
 #pragma unroll 4
   for (int c = slice; c < C; c += CS) {
     const float* xc = xb + (size_t)c * HW;
@@ -360,6 +414,11 @@ __global__ __launch_bounds__(256) void warp_bwd_kernel(const float* __restrict__
     const float* xb = x + (size_t)b * C * HW;
     const float* gb = gout + (size_t)b * C * HW + (valid ? p : 0);
     float* gxb = WANT_GX ? gx + (size_t)b * C * HW : nullptr;
+    // corner pairs (pair_tap) measured no faster here (L4 56.9 vs 54.5 us,
+    // profiles/ab_r04/warp_corner_pairs.json): the filing pass is not gather-bound
+    const bool pairs = USF_WARP_BWD_PAIR && W >= 2;
+    const PairTap q = pair_tap(tp, W);
+    const auto rsx = sample_rsrc(xb, 4 * C * HW);
 #pragma unroll 2
     for (int c = slice; c < C; c += CS) {
       const float go = valid ? gb[(size_t)c * HW] : 0.f;
@@ -369,11 +428,16 @@ __global__ __launch_bounds__(256) void warp_bwd_kernel(const float* __restrict__
         scatter_row(gc, tp.o_sw, tp.o_se, tp.m_sw, tp.m_se, go * wsw, go * wse, rs);
       }
       if (WANT_GF && valid) {
-        const float* xc = xb + (size_t)c * HW;
-        const float vnw = tp.m_nw ? xc[tp.o_nw] : 0.f;
-        const float vne = tp.m_ne ? xc[tp.o_ne] : 0.f;
-        const float vsw = tp.m_sw ? xc[tp.o_sw] : 0.f;
-        const float vse = tp.m_se ? xc[tp.o_se] : 0.f;
+        float vnw, vne, vsw, vse;
+        if (pairs) {
+          pair_corners(rsx, q, tp, 4u * (unsigned)(c * HW), vnw, vne, vsw, vse);
+        } else {
+          const float* xc = xb + (size_t)c * HW;
+          vnw = tp.m_nw ? xc[tp.o_nw] : 0.f;
+          vne = tp.m_ne ? xc[tp.o_ne] : 0.f;
+          vsw = tp.m_sw ? xc[tp.o_sw] : 0.f;
+          vse = tp.m_se ? xc[tp.o_se] : 0.f;
+        }
         dix += ((vne - vnw) * tp.s + (vse - vsw) * tp.n) * go;
         diy += ((vsw - vnw) * tp.e + (vse - vne) * tp.w) * go;
       }
