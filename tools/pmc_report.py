@@ -41,7 +41,10 @@ for (name, grid, wg), c in data.items():
     if "SQ_INSTS_VALU" in c:
         line += (f" | valuI={c['SQ_INSTS_VALU']:.3g} ldsI={c['SQ_INSTS_LDS']:.3g} saluI={c['SQ_INSTS_SALU']:.3g}"
                  f" bankconf={c['SQ_LDS_BANK_CONFLICT']:.3g} waitLDS={c['SQ_WAIT_INST_LDS']:.3g}")
-        if "GRBM_GUI_ACTIVE" in c and c.get("_dur_us"):
+        # effective clock = GRBM_GUI_ACTIVE / 8 XCDs / wall time; the quotient reads
+        # high for dispatches under ~0.3 ms (MI355X_MICROARCH.md, DVFS give-back), so
+        # it is only printed for longer ones (the r03 report showed 2.4-5.9 "GHz")
+        if "GRBM_GUI_ACTIVE" in c and c.get("_dur_us", 0) >= 300:
             line += f" clk={c['GRBM_GUI_ACTIVE'] / 8 / c['_dur_us'] / 1e3:.2f}GHz"
     if "FETCH_SIZE" in c:
         line += f" | FETCH={c['FETCH_SIZE'] / 1024:.1f}MB"

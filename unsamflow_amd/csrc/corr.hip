@@ -928,6 +928,11 @@ struct BwdCfg {
 // One (tile, channel group) of gx1 (G2 == false: from g and x2) or gx2
 // (G2 == true: from g and x1; mirrored indices).
 
+// 1: the backward's stage-0 x DMA goes out before the g slice and the first
+// barrier waits only for it (corr_bwd_tile); 0: both waited for (vmcnt(0)).
+#ifndef USF_BWD_EARLY
+#define USF_BWD_EARLY 1
+#endif
 // Occupancy target of the backward kernels (see corr_bwd_kernel).
 #ifndef USF_BWD_WAVES_PER_EU
 #define USF_BWD_WAVES_PER_EU 3
@@ -1050,11 +1055,7 @@ __device__ __forceinline__ void bwd_stage(const float (&gv)[DYW][K][PX], const f
       // compile-time true when the waves' rows tile K exactly (NW * DYW == K):
       // no per-row branch, so the compiler overlaps one row's ds_reads with the
       // previous row's FMAs (L4 75.4 -> 70.6 us, profiles/ab_r02)
-#if defined(USF_BWD_PROBE) && USF_BWD_PROBE == 5
-      if (ep.slope == 12345.f) {  // probe: no FMAs (timing only)
-#else
       if (NW * DYW == K || dy < K) {
-#endif
         const int rs = G2 ? (2 * D - dy) : dy;
         float w[WIN];
         lds_read<B64>(cur + c * P + (r + rs) * S + q * PX, w);
@@ -1158,36 +1159,6 @@ __device__ __forceinline__ void corr_bwd_tile(float* sm, const float* __restrict
 
   const int HW = H * W;
   const float* xsb = xs + (size_t)b * C * HW;
-  // g of sample b at b * ep.g_bstride: a channel slice of the concat gradient,
-  // or the dense [B,K*K,H,W] tensor
-  float gv[DYW][2 * D + 1][PX];
-  bwd_load_g<D, PX, SEGX, NW, CC, V, G2, AM>(gv, g + (size_t)b * ep.g_bstride, ep, b, wave, y, xb, H, W);
-  USF_TRACE_VMWAIT();
-  USF_TRACE_AT(1);
-#ifdef USF_BWD_PROBE
-  // timing probes only (tools/ab_build.py): 1 = no g loads (runtime constants),
-  // 2 = g loads and the output store only (no channel stages)
-  if constexpr (USF_BWD_PROBE == 1) {
-#pragma unroll
-    for (int t = 0; t < DYW; ++t)
-#pragma unroll
-      for (int dx = 0; dx < 2 * D + 1; ++dx)
-#pragma unroll
-        for (int i = 0; i < PX; ++i) gv[t][dx][i] = ep.slope * (float)(t + dx + i);
-  }
-  if constexpr (USF_BWD_PROBE == 2) {
-    float sacc = 0.f;
-#pragma unroll
-    for (int t = 0; t < DYW; ++t)
-#pragma unroll
-      for (int dx = 0; dx < 2 * D + 1; ++dx)
-#pragma unroll
-        for (int i = 0; i < PX; ++i) sacc += gv[t][dx][i];
-    if (y < H && xb < W) gx[(size_t)b * C * HW + (size_t)(cbeg + wave) * HW + y * W + xb] = sacc;
-    return;
-  }
-#endif
-
   typename F::X sx;
   sx.init(wave, lane, y0 - D, x0 - D, H, W);
   const rsrc_t rx = plane_rsrc(xsb, true, C * HW * 4);
@@ -1196,8 +1167,22 @@ __device__ __forceinline__ void corr_bwd_tile(float* sm, const float* __restrict
   const float cf = 1.f / (float)C, fc = (float)C;  // bwd_combine's scale (exact: power-of-two C only)
   const bool pow2 = (C & (C - 1)) == 0;
   float* gxb = gx + (size_t)b * C * HW;
+  // Stage 0's x DMA goes out before the g slice, and the first barrier waits
+  // only for it: vmcnt(DYW * K) leaves the youngest DYW * K loads (at most the
+  // slice's) in flight, so the FMAs of displacement row t wait only for that
+  // row's g loads (hipcc's per-register waits) and the slice's HBM burst
+  // overlaps the first stage.
   dma_stage(cbeg, sm);
-  dma_wait_all();
+  // g of sample b at b * ep.g_bstride: a channel slice of the concat gradient,
+  // or the dense [B,K*K,H,W] tensor
+  float gv[DYW][2 * D + 1][PX];
+  bwd_load_g<D, PX, SEGX, NW, CC, V, G2, AM>(gv, g + (size_t)b * ep.g_bstride, ep, b, wave, y, xb, H, W);
+  USF_TRACE_VMWAIT();
+  USF_TRACE_AT(1);
+  if constexpr (USF_BWD_EARLY)
+    asm volatile("s_waitcnt vmcnt(%0)" ::"i"(DYW * (2 * D + 1)) : "memory");
+  else
+    dma_wait_all();
   __syncthreads();
   USF_TRACE_AT(2);
   int st = 0;
@@ -1210,9 +1195,6 @@ __device__ __forceinline__ void corr_bwd_tile(float* sm, const float* __restrict
     dma_wait_all();
     __syncthreads();  // partials complete; next stage's image landed
     USF_TRACE_AT(5 + 4 * st);
-#if defined(USF_BWD_PROBE) && USF_BWD_PROBE == 3
-    continue;  // probe: no combine, no second barrier (timing only)
-#endif
     bwd_combine<D, PX, SEGX, NW, CC, V>(red, gxb, tid, NT, c0, cend, y0, x0, H, W, cf, fc, pow2);
     __syncthreads();  // partial slices free for the next stage
     USF_TRACE_AT(6 + 4 * st);
