@@ -310,6 +310,14 @@ struct FwdCfg {
   static_assert(V == 1 || L::X4, "16-byte DMA needs the 4-aligned layout");
 };
 
+// 1: partial-column tiles are dispatched last (corr_fwd_kernel); 0: the
+// XCD-contiguous order for every grid
+#ifndef USF_FWD_EDGE_LAST
+#define USF_FWD_EDGE_LAST 1
+#endif
+#ifndef USF_FWD_EDGE_CHUNK
+#define USF_FWD_EDGE_CHUNK 8
+#endif
 template <int D, int PX, int SEGX, int NDY, int CC, int V, int CS = 1>
 __global__ __launch_bounds__(64 * NDY * CS) void corr_fwd_kernel(const float* __restrict__ x1,
                                                                  const float* __restrict__ x2,
@@ -329,10 +337,39 @@ __global__ __launch_bounds__(64 * NDY * CS) void corr_fwd_kernel(const float* __
   const int slice = wall / NDY;                                      // channel slice (uniform)
   const int wave = wall - slice * NDY;                               // displacement row in the group
   // work item: displacement-row group fastest, then tile, then (sample, channel group)
-  const int w = xcd_remap(linear_block(), gridDim.x * gridDim.y * gridDim.z);
-  const int dyb = (w % F::NDYG) * NDY;
-  const int tile = (w / F::NDYG) % gridDim.y;
-  const int bz = w / (F::NDYG * gridDim.y);
+  const int nitems = gridDim.x * gridDim.y * gridDim.z;
+  int dyb, tile, bz;
+  const int tiles_y = gridDim.y / tiles_x;
+  if (USF_FWD_EDGE_LAST && (W % TW) != 0 && tiles_x > 1) {
+    // Partial-column tiles (the image's right edge, about half the work of a
+    // full tile) are dispatched LAST, in chunks of consecutive items per XCD
+    // (xcd_chunk keeps dispatch order at chunk granularity): when the grid is a
+    // little over one resident round (KITTI L4 at batch 16: 896 workgroups for
+    // 768 slots, 128 of them edge tiles), the second round is the cheap one.
+    const int u = xcd_chunk(linear_block(), nitems, USF_FWD_EDGE_CHUNK);
+    const int g = u % F::NDYG, pi = u / F::NDYG;
+    const int tf = tiles_y * (tiles_x - 1);     // full-column tiles per (sample, group)
+    const int nfull = (int)(gridDim.z) * tf;
+    int tx, ty;
+    if (pi < nfull) {
+      bz = pi / tf;
+      const int t = pi - bz * tf;
+      ty = t / (tiles_x - 1);
+      tx = t - ty * (tiles_x - 1);
+    } else {
+      const int e = pi - nfull;
+      bz = e / tiles_y;
+      ty = e - bz * tiles_y;
+      tx = tiles_x - 1;
+    }
+    dyb = g * NDY;
+    tile = ty * tiles_x + tx;
+  } else {
+    const int w = xcd_remap(linear_block(), nitems);
+    dyb = (w % F::NDYG) * NDY;
+    tile = (w / F::NDYG) % gridDim.y;
+    bz = w / (F::NDYG * gridDim.y);
+  }
   const int G = ep.groups;
   const int b = bz / G, grp = bz - b * G;
   // channel range of this workgroup (whole C without a split)
