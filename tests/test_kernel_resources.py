@@ -5,6 +5,7 @@ rests on occupancy: the default backward tile <d=4, PX=4, SEGX=8, NW=3, CC=4>
 must stay within 168 VGPRs (3 waves/SIMD) and 40 KB of LDS (4 workgroups of
 3 waves per CU), and no kernel may spill to scratch.
 """
+import re
 import shutil
 
 import pytest
@@ -30,7 +31,8 @@ def test_no_kernel_spills(corr_resources):
 
 
 def test_default_backward_tile_occupancy(corr_resources):
-    default = [r for r in corr_resources if "corr_bwd_kernelILi4ELi4ELi8ELi3ELi4E" in r[0]]
+    # <4,4,8,3,4, V, MODE, AM, NB = 2>
+    default = [r for r in corr_resources if re.search(r"corr_bwd_kernelILi4ELi4ELi8ELi3ELi4ELi\dELi\dELb\dELi2E", r[0])]
     assert default, "default backward instantiation missing"
     for name, vgpr, lds, _ in default:
         assert vgpr <= 168, (name, vgpr)
@@ -41,7 +43,8 @@ def test_large_level_forward_occupancy(corr_resources):
     """The L3/L4 forward tile <d=4, PX=4, SEGX=8, NDY=9, CC=4> keeps its 7
     waves/SIMD with the sign-mask epilogue (a per-bit bounds test in the
     epilogue once raised it from 65 to 101 VGPRs and slowed L4 by ~25%)."""
-    fwd = [r for r in corr_resources if "corr_fwd_kernelILi4ELi4ELi8ELi9ELi4E" in r[0]]
+    # <4,4,8,9,4, V, CS = 1>
+    fwd = [r for r in corr_resources if re.search(r"corr_fwd_kernelILi4ELi4ELi8ELi9ELi4ELi\dELi1EE", r[0])]
     assert fwd, "large-level forward instantiation missing"
     for name, vgpr, _, _ in fwd:
         assert vgpr <= 72, (name, vgpr)

@@ -9,8 +9,8 @@
 // Caveat: the stamps cost registers (the fused backward goes from 163 to 189
 // VGPRs, i.e. 2 instead of 3 waves/SIMD), so occupancy and absolute times of a
 // traced run differ from the library's; use it for the phase breakdown.
-// Build: hipcc -O3 -std=c++17 --offload-arch=gfx950 -DUSF_TRACE -I unsamflow_amd/csrc
-//        -o tools/probes/corr_trace tools/probes/corr_trace.hip; run: tools/gpu_trace.sh
+// Build: hipcc -O3 -std=c++17 --offload-arch=gfx950 -DUSF_TRACE -I unsamflow_amd/csrc -I include
+//        -o tools/probes/bin/corr_trace tools/probes/corr_trace.hip; run: tools/gpu_trace.sh
 // Usage: corr_trace fwd|bwd B C H W [variant]
 #include <algorithm>
 #include <cstdio>
@@ -133,16 +133,17 @@ int main(int argc, char** argv) {
   printf("  wave duration p10/p50/p90/max %.2f/%.2f/%.2f/%.2f us\n", pct(dur, .1), pct(dur, .5),
          pct(dur, .9), pct(dur, 1));
   printf("  max resident waves per CU %d, per SIMD %d\n", max_res(per_cu), max_res(per_simd));
-  // fwd: [1] prologue+first DMA, then per stage: DMA issue, compute, DMA drain, barrier
-  // bwd: [1] g load, [2] first DMA, then per stage: DMA issue, compute, drain+barrier, flush+barrier
-  const int first = fwd ? 2 : 3;
+  // fwd: [1] prologue DMA issue, then per stage: loop, DMA wait, barrier + next DMA issue, compute
+  // bwd: [1] prologue DMA + g slice issue, [2] -, then per stage: DMA wait, barrier + next DMA
+  //      issue, compute, barrier, combine (the combine of stage s is the next stage's first phase)
+  const int first = fwd ? 2 : 3, stride = fwd ? 4 : 5;
   printf("  prologue (median us):");
   for (int k = 1; k < first; ++k) printf(" [%d] %.2f", k, pct(ph[k], .5));
-  printf("\n  per stage (median us) issue/compute/%s/%s:\n", fwd ? "drain" : "drain+bar",
-         fwd ? "barrier" : "flush+bar");
-  for (int st = 0; first + 4 * st + 3 < S - 1 && !ph[first + 4 * st].empty(); ++st) {
+  printf("\n  per stage (median us) %s:\n",
+         fwd ? "loop/wait/bar+issue/compute" : "wait/bar+issue/compute/bar/combine");
+  for (int st = 0; first + stride * st + stride - 1 < S - 1 && !ph[first + stride * st].empty(); ++st) {
     printf("    stage %2d:", st);
-    for (int k = 0; k < 4; ++k) printf(" %6.2f", pct(ph[first + 4 * st + k], .5));
+    for (int k = 0; k < stride; ++k) printf(" %6.2f", pct(ph[first + stride * st + k], .5));
     printf("\n");
   }
   return 0;

@@ -318,6 +318,15 @@ struct FwdCfg {
 #ifndef USF_FWD_EDGE_CHUNK
 #define USF_FWD_EDGE_CHUNK 8
 #endif
+// ... for grids of at least this many workgroups (smaller ones fit one round,
+// where the reorder measured slower: config 2 23.1 -> 26.3 us warm)
+#ifndef USF_FWD_EDGE_MIN
+#define USF_FWD_EDGE_MIN 512
+#endif
+
+template <int N>
+__device__ __forceinline__ void dma_wait_le() { asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory"); }
+
 template <int D, int PX, int SEGX, int NDY, int CC, int V, int CS = 1>
 __global__ __launch_bounds__(64 * NDY * CS) void corr_fwd_kernel(const float* __restrict__ x1,
                                                                  const float* __restrict__ x2,
@@ -340,7 +349,7 @@ __global__ __launch_bounds__(64 * NDY * CS) void corr_fwd_kernel(const float* __
   const int nitems = gridDim.x * gridDim.y * gridDim.z;
   int dyb, tile, bz;
   const int tiles_y = gridDim.y / tiles_x;
-  if (USF_FWD_EDGE_LAST && (W % TW) != 0 && tiles_x > 1) {
+  if (USF_FWD_EDGE_LAST && (W % TW) != 0 && tiles_x > 1 && nitems >= USF_FWD_EDGE_MIN) {
     // Partial-column tiles (the image's right edge, about half the work of a
     // full tile) are dispatched LAST, in chunks of consecutive items per XCD
     // (xcd_chunk keeps dispatch order at chunk granularity): when the grid is a
@@ -401,15 +410,21 @@ __global__ __launch_bounds__(64 * NDY * CS) void corr_fwd_kernel(const float* __
 #pragma unroll
     for (int i = 0; i < PX; ++i) acc[j][i] = 0.f;
 
+  // Two stage images: each iteration waits for stage st, then (after the
+  // barrier: every wave is done with stage st - 1's image) refills that image
+  // with stage st + 1, in flight while stage st is summed. (A deeper ring, NB - 1
+  // stages in flight, was slower at every shape in rounds 3 and 4: §4.2.)
+  const int nst = (cend - cbeg + CC - 1) / CC;
   dma_stage(cbeg, sm);
-  dma_wait_all();
-  __syncthreads();
   USF_TRACE_AT(1);
-  int st = 0;
-  for (int c0 = cbeg; c0 < cend; c0 += CC, ++st) {
-    const float* cur = sm + (st & 1) * STAGE;
-    if (c0 + CC < cend) dma_stage(c0 + CC, sm + ((st + 1) & 1) * STAGE);  // in flight during FMAs
+  for (int st = 0; st < nst; ++st) {
     USF_TRACE_AT(2 + 4 * st);
+    dma_wait_all();
+    USF_TRACE_AT(3 + 4 * st);
+    __syncthreads();
+    if (st + 1 < nst) dma_stage(cbeg + (st + 1) * CC, sm + ((st + 1) & 1) * STAGE);  // in flight during FMAs
+    const float* cur = sm + (st & 1) * STAGE;
+    USF_TRACE_AT(4 + 4 * st);
     if (active) {
       const float* p1 = cur + r * S + q * PX;
       const float* p2 = cur + N1 + (r + wave) * S + q * PX;
@@ -428,10 +443,6 @@ __global__ __launch_bounds__(64 * NDY * CS) void corr_fwd_kernel(const float* __
           for (int i = 0; i < PX; ++i) acc[dx][i] = fmaf(a[i], w[i + dx], acc[dx][i]);
       }
     }
-    USF_TRACE_AT(3 + 4 * st);
-    dma_wait_all();
-    USF_TRACE_AT(4 + 4 * st);
-    __syncthreads();
     USF_TRACE_AT(5 + 4 * st);
   }
 
@@ -443,8 +454,9 @@ __global__ __launch_bounds__(64 * NDY * CS) void corr_fwd_kernel(const float* __
     for (long long i = (long long)linear_block() * blockDim.x + threadIdx.x; i < nw; i += nt) ep.mask[i] = 0ull;
   }
   if constexpr (CS > 1) {
-    // slices 1.. hand their sums to slice 0 through the (now idle) stage
-    // buffers; slice 0 adds them in slice order and runs the epilogue
+    // slices 1.. hand their sums to slice 0 through the stage buffers (idle
+    // after this barrier); slice 0 adds them in slice order and runs the epilogue
+    __syncthreads();
     float* xa = sm + (wave * K * PX) * 64 + lane;
     if (slice > 0 && active) {
 #pragma unroll
@@ -937,12 +949,13 @@ hipError_t fwd_dispatch(const float* x1, const float* x2, float* out, int B, int
 #ifndef USF_BWD_VECG
 #define USF_BWD_VECG 1
 #endif
-template <int D, int PX, int SEGX, int NW, int CC, int V>
+template <int D, int PX, int SEGX, int NW, int CC, int V, int NB = 2>
 struct BwdCfg {
   static constexpr int K = 2 * D + 1;
   static constexpr int TW = SEGX * PX;
   static constexpr int TH = 64 / SEGX;
   static constexpr int NT = 64 * NW;
+  static constexpr int NW_ = NW;
   static constexpr int DYW = (K + NW - 1) / NW;      // displacement rows per wave
   using L = Layout<PX, SEGX, D>;
   static constexpr int R = TH + 2 * D;               // staged rows
@@ -953,11 +966,15 @@ struct BwdCfg {
   static constexpr int WIN = round_up(PX + 2 * D, 4);
   static constexpr int XIMG = X::N;
   static constexpr int RED = NW * CC * TH * TW;      // per-wave partial sums
-  // <4,4,8,3,4>: 40 KB, so four workgroups fit the 160 KB LDS of a CU
-  // two x image buffers: the DMA of stage s + 1 is in flight during stage s.
-  // A third buffer (two stages in flight, 48 KB: 3 workgroups per CU) was
-  // slower: L4 76.2 vs 67.8 us (profiles/ab_r02/bwd_nbuf.json)
-  static constexpr int LDSN = 2 * XIMG + RED;
+  // <4,4,8,3,4>: 36 KB, so four workgroups fit the 160 KB LDS of a CU.
+  // NB x image buffers in a ring: the DMA of stages s + 1 .. s + NB - 1 is in
+  // flight during stage s. At L4 a third buffer (48 KB: 3 workgroups per CU)
+  // was slower, 76.2 vs 67.8 us (profiles/ab_r02/bwd_nbuf.json); four buffers
+  // pay on small grids, whose channel loops are short (bwd_dispatch).
+  static constexpr int LDSN = NB * XIMG + RED;
+  static constexpr int CC_ = CC;
+  // resident workgroups per CU the LDS allows (at most the 3 the VGPRs allow)
+  static constexpr int PER_CU = (160 * 1024 / (LDSN * 4)) < 3 ? (160 * 1024 / (LDSN * 4)) : 3;
   static_assert(PX % 4 == 0, "PX must be a multiple of 4");
   static_assert(V == 1 || L::X4, "16-byte DMA needs the 4-aligned layout");
 };
@@ -1170,17 +1187,28 @@ __device__ __forceinline__ void bwd_combine(const float* red, float* gxb, int t1
 
 // One (tile, channel group) of gx1 (G2 == false: from g and x2) or gx2
 // (G2 == true: from g and x1; mirrored indices).
-template <int D, int PX, int SEGX, int NW, int CC, int V, bool G2, bool AM>
+// Wait until at most KS stages of this wave's x DMA plus EXTRA younger loads
+// are outstanding. A wave owns the J-th chunk slot of the image or not
+// (StageImg::load), so it issues one of two per-stage counts.
+template <class F, int KS, int EXTRA>
+__device__ __forceinline__ void bwd_wait_stages(int wave) {
+  constexpr int J = F::X::J, CC = F::CC_;
+  static_assert(KS * CC * J + EXTRA <= 63, "vmcnt holds 6 bits");
+  if (wave + (J - 1) * F::NW_ < F::X::CHP) dma_wait_le<KS * CC * J + EXTRA>();
+  else dma_wait_le<KS * CC * (J - 1) + EXTRA>();
+}
+
+template <int D, int PX, int SEGX, int NW, int CC, int V, bool G2, bool AM, int NB>
 __device__ __forceinline__ void corr_bwd_tile(float* sm, const float* __restrict__ xs,
                                               const float* __restrict__ g,
                                               float* __restrict__ gx, int tile, int group, int b,
                                               int C, int H, int W, int tiles_x, int cg,
                                               const BwdEpi& ep) {
-  using F = BwdCfg<D, PX, SEGX, NW, CC, V>;
+  using F = BwdCfg<D, PX, SEGX, NW, CC, V, NB>;
   constexpr int K = F::K, TW = F::TW, TH = F::TH, NT = F::NT;
   constexpr int DYW = F::DYW, XIMG = F::XIMG;
   (void)K;
-  float* red = sm + 2 * XIMG;
+  float* red = sm + NB * XIMG;
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -1204,37 +1232,47 @@ __device__ __forceinline__ void corr_bwd_tile(float* sm, const float* __restrict
   const float cf = 1.f / (float)C, fc = (float)C;  // bwd_combine's scale (exact: power-of-two C only)
   const bool pow2 = (C & (C - 1)) == 0;
   float* gxb = gx + (size_t)b * C * HW;
-  // Stage 0's x DMA goes out before the g slice, and the first barrier waits
-  // only for it: vmcnt(DYW * K) leaves the youngest DYW * K loads (at most the
-  // slice's) in flight, so the FMAs of displacement row t wait only for that
-  // row's g loads (hipcc's per-register waits) and the slice's HBM burst
+  // The x DMA of stages 0 .. NB-2 goes out before the g slice, and the first
+  // barrier waits only for stage 0: vmcnt leaves the younger stages and the
+  // DYW * K g loads in flight, so the FMAs of displacement row t wait only for
+  // that row's g loads (hipcc's per-register waits) and the slice's HBM burst
   // overlaps the first stage.
-  dma_stage(cbeg, sm);
+  const int nst = (cend - cbeg + CC - 1) / CC;
+#pragma unroll
+  for (int i = 0; i < NB - 1; ++i)
+    if (i < nst) dma_stage(cbeg + i * CC, sm + i * XIMG);
   // g of sample b at b * ep.g_bstride: a channel slice of the concat gradient,
   // or the dense [B,K*K,H,W] tensor
   float gv[DYW][2 * D + 1][PX];
   bwd_load_g<D, PX, SEGX, NW, CC, V, G2, AM>(gv, g + (size_t)b * ep.g_bstride, ep, b, wave, y, xb, H, W);
   USF_TRACE_VMWAIT();
   USF_TRACE_AT(1);
-  if constexpr (USF_BWD_EARLY)
-    asm volatile("s_waitcnt vmcnt(%0)" ::"i"(DYW * (2 * D + 1)) : "memory");
-  else
-    dma_wait_all();
-  __syncthreads();
-  USF_TRACE_AT(2);
-  int st = 0;
-  for (int c0 = cbeg; c0 < cend; c0 += CC, ++st) {
-    const float* cur = sm + (st & 1) * XIMG;
-    if (c0 + CC < cend) dma_stage(c0 + CC, sm + ((st + 1) & 1) * XIMG);
-    USF_TRACE_AT(3 + 4 * st);
+  // ring: stage st in slot st % NB. Each iteration waits for stage st, then
+  // (after the barrier: every wave is done with stage st - 1's slot and the
+  // previous combine's partials) refills that slot with stage st + NB - 1.
+  int rd = 0, wr = NB - 1;
+  for (int st = 0; st < nst; ++st) {
+    USF_TRACE_AT(2 + 5 * st);
+    if (st == 0 && USF_BWD_EARLY) {
+      if (NB == 2 || nst >= NB - 1) bwd_wait_stages<F, NB - 2, DYW * K>(wave);
+      else dma_wait_all();
+    } else if (NB > 2 && st + NB - 2 < nst) {
+      bwd_wait_stages<F, NB - 2, 0>(wave);
+    } else {
+      dma_wait_all();
+    }
+    USF_TRACE_AT(3 + 5 * st);
+    __syncthreads();  // stage st landed; partial slices free
+    if (st + NB - 1 < nst) dma_stage(cbeg + (st + NB - 1) * CC, sm + wr * XIMG);
+    const float* cur = sm + rd * XIMG;
+    rd = rd + 1 == NB ? 0 : rd + 1;
+    wr = wr + 1 == NB ? 0 : wr + 1;
+    USF_TRACE_AT(4 + 5 * st);
     bwd_stage<D, PX, SEGX, NW, CC, V, G2>(gv, cur, red + wave * (CC * TH * TW) + lane * PX, wave, r, q, ep);
-    USF_TRACE_AT(4 + 4 * st);
-    dma_wait_all();
-    __syncthreads();  // partials complete; next stage's image landed
-    USF_TRACE_AT(5 + 4 * st);
-    bwd_combine<D, PX, SEGX, NW, CC, V>(red, gxb, tid, NT, c0, cend, y0, x0, H, W, cf, fc, pow2);
-    __syncthreads();  // partial slices free for the next stage
-    USF_TRACE_AT(6 + 4 * st);
+    USF_TRACE_AT(5 + 5 * st);
+    __syncthreads();  // partials complete
+    USF_TRACE_AT(6 + 5 * st);
+    bwd_combine<D, PX, SEGX, NW, CC, V>(red, gxb, tid, NT, cbeg + st * CC, cend, y0, x0, H, W, cf, fc, pow2);
   }
 }
 
@@ -1246,7 +1284,7 @@ __device__ __forceinline__ void corr_bwd_tile(float* sm, const float* __restrict
 // 40 KB LDS, i.e. 3 waves/SIMD = 4 resident workgroups of 3 waves per CU.
 // amdgpu_waves_per_eu(3) pins the VGPR target: without it, allocation for the
 // two inlined direction bodies flips between 163 and 231 on unrelated edits.
-template <int D, int PX, int SEGX, int NW, int CC, int V, int MODE, bool AM>
+template <int D, int PX, int SEGX, int NW, int CC, int V, int MODE, bool AM, int NB>
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(USF_BWD_WAVES_PER_EU))) void corr_bwd_kernel(const float* __restrict__ x1,
                                                            const float* __restrict__ x2,
                                                            const float* __restrict__ g,
@@ -1254,7 +1292,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(USF_BWD
                                                            float* __restrict__ gx2, int B, int C,
                                                            int H, int W, int tiles_x, int cg,
                                                            BwdEpi ep) {
-  __shared__ __attribute__((aligned(16))) float sm[BwdCfg<D, PX, SEGX, NW, CC, V>::LDSN];
+  __shared__ __attribute__((aligned(16))) float sm[BwdCfg<D, PX, SEGX, NW, CC, V, NB>::LDSN];
   USF_TRACE_AT(0);
   USF_TRACE_HWID();
   // work item: channel group fastest (the groups of a tile share its g planes),
@@ -1299,15 +1337,15 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(USF_BWD
     b = w / (gridDim.x * gridDim.y);
   }
   if constexpr (MODE == 1) {
-    corr_bwd_tile<D, PX, SEGX, NW, CC, V, false, AM>(sm, x2, g, gx1, tile, group, b, C, H, W, tiles_x, cg, ep);
+    corr_bwd_tile<D, PX, SEGX, NW, CC, V, false, AM, NB>(sm, x2, g, gx1, tile, group, b, C, H, W, tiles_x, cg, ep);
   } else if constexpr (MODE == 2) {
-    corr_bwd_tile<D, PX, SEGX, NW, CC, V, true, AM>(sm, x1, g, gx2, tile, group, b, C, H, W, tiles_x, cg, ep);
+    corr_bwd_tile<D, PX, SEGX, NW, CC, V, true, AM, NB>(sm, x1, g, gx2, tile, group, b, C, H, W, tiles_x, cg, ep);
   } else {
     if (b >= B)
-      corr_bwd_tile<D, PX, SEGX, NW, CC, V, true, AM>(sm, x1, g, gx2, tile, group, b - B, C, H, W,
+      corr_bwd_tile<D, PX, SEGX, NW, CC, V, true, AM, NB>(sm, x1, g, gx2, tile, group, b - B, C, H, W,
                                                       tiles_x, cg, ep);
     else
-      corr_bwd_tile<D, PX, SEGX, NW, CC, V, false, AM>(sm, x2, g, gx1, tile, group, b, C, H, W,
+      corr_bwd_tile<D, PX, SEGX, NW, CC, V, false, AM, NB>(sm, x2, g, gx1, tile, group, b, C, H, W,
                                                        tiles_x, cg, ep);
   }
 }
@@ -1320,51 +1358,53 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(USF_BWD
 #endif
 constexpr int kBwdTargetWorkgroups = USF_BWD_TARGET_WG;
 
-template <int D, int PX, int SEGX, int NW, int CC, int V, int MODE>
+template <int D, int PX, int SEGX, int NW, int CC, int V, int MODE, int NB>
 hipError_t launch_bwd_mode(const float* x1, const float* x2, const float* g, float* gx1,
                            float* gx2, int B, int C, int H, int W, hipStream_t s, BwdEpi ep) {
-  using F = BwdCfg<D, PX, SEGX, NW, CC, V>;
+  using F = BwdCfg<D, PX, SEGX, NW, CC, V, NB>;
   const int dirs = MODE == 3 ? 2 : 1;
   const int tiles_x = (W + F::TW - 1) / F::TW;
   const int tiles_y = (H + F::TH - 1) / F::TH;
   const long units = (long)tiles_x * tiles_y * B * dirs;
-  int groups = (int)((kBwdTargetWorkgroups + units - 1) / units);
+  // one resident round: 768 at 3 workgroups per CU, fewer for a deeper ring
+  const long target = (long)kBwdTargetWorkgroups * F::PER_CU / 3;
+  int groups = (int)((target + units - 1) / units);
   groups = max(1, min(groups, (C + CC - 1) / CC));
   const int cg = round_up((C + groups - 1) / groups, CC);
   dim3 grid(tiles_x * tiles_y, (C + cg - 1) / cg, B * dirs);
   if constexpr (PX == 4) {
     if (ep.mask) {
-      hipLaunchKernelGGL((corr_bwd_kernel<D, PX, SEGX, NW, CC, V, MODE, true>), grid, dim3(F::NT), 0, s,
+      hipLaunchKernelGGL((corr_bwd_kernel<D, PX, SEGX, NW, CC, V, MODE, true, NB>), grid, dim3(F::NT), 0, s,
                          x1, x2, g, gx1, gx2, B, C, H, W, tiles_x, cg, ep);
       return hipGetLastError();
     }
   }
   if (ep.mask) return hipErrorInvalidValue;  // 4-pixel runs only
-  hipLaunchKernelGGL((corr_bwd_kernel<D, PX, SEGX, NW, CC, V, MODE, false>), grid, dim3(F::NT), 0, s, x1,
+  hipLaunchKernelGGL((corr_bwd_kernel<D, PX, SEGX, NW, CC, V, MODE, false, NB>), grid, dim3(F::NT), 0, s, x1,
                      x2, g, gx1, gx2, B, C, H, W, tiles_x, cg, ep);
   return hipGetLastError();
 }
 
-template <int D, int PX, int SEGX, int NW, int CC, int V>
+template <int D, int PX, int SEGX, int NW, int CC, int V, int NB>
 hipError_t launch_bwd_v(const float* x1, const float* x2, const float* g, float* gx1, float* gx2,
                         int B, int C, int H, int W, hipStream_t s, BwdEpi ep) {
   if (gx1 && gx2)
-    return launch_bwd_mode<D, PX, SEGX, NW, CC, V, 3>(x1, x2, g, gx1, gx2, B, C, H, W, s, ep);
+    return launch_bwd_mode<D, PX, SEGX, NW, CC, V, 3, NB>(x1, x2, g, gx1, gx2, B, C, H, W, s, ep);
   hipError_t e = hipSuccess;
-  if (gx1) e = launch_bwd_mode<D, PX, SEGX, NW, CC, V, 1>(x1, x2, g, gx1, gx2, B, C, H, W, s, ep);
+  if (gx1) e = launch_bwd_mode<D, PX, SEGX, NW, CC, V, 1, NB>(x1, x2, g, gx1, gx2, B, C, H, W, s, ep);
   if (e == hipSuccess && gx2)
-    e = launch_bwd_mode<D, PX, SEGX, NW, CC, V, 2>(x1, x2, g, gx1, gx2, B, C, H, W, s, ep);
+    e = launch_bwd_mode<D, PX, SEGX, NW, CC, V, 2, NB>(x1, x2, g, gx1, gx2, B, C, H, W, s, ep);
   return e;
 }
 
-template <int D, int PX = 4, int SEGX = 8, int NW = 3, int CC = 4>
+template <int D, int PX = 4, int SEGX = 8, int NW = 3, int CC = 4, int NB = 2>
 hipError_t launch_bwd(const float* x1, const float* x2, const float* g, float* gx1, float* gx2,
                       int B, int C, int H, int W, hipStream_t s, BwdEpi ep) {
   if constexpr (Layout<PX, SEGX, D>::X4) {
     if (W % 4 == 0)
-      return launch_bwd_v<D, PX, SEGX, NW, CC, 4>(x1, x2, g, gx1, gx2, B, C, H, W, s, ep);
+      return launch_bwd_v<D, PX, SEGX, NW, CC, 4, NB>(x1, x2, g, gx1, gx2, B, C, H, W, s, ep);
   }
-  return launch_bwd_v<D, PX, SEGX, NW, CC, 1>(x1, x2, g, gx1, gx2, B, C, H, W, s, ep);
+  return launch_bwd_v<D, PX, SEGX, NW, CC, 1, NB>(x1, x2, g, gx1, gx2, B, C, H, W, s, ep);
 }
 
 hipError_t bwd_candidate_d4(int i, const float* x1, const float* x2, const float* g, float* gx1,
@@ -1374,10 +1414,23 @@ hipError_t bwd_candidate_d4(int i, const float* x1, const float* x2, const float
     case 1: return launch_bwd<4, 4, 8, 3, 8>(x1, x2, g, gx1, gx2, B, C, H, W, s, ep);
     case 2: return launch_bwd<4, 4, 8, 9, 4>(x1, x2, g, gx1, gx2, B, C, H, W, s, ep);
     case 3: return launch_bwd<4, 4, 8, 9, 8>(x1, x2, g, gx1, gx2, B, C, H, W, s, ep);
+    case 4: return launch_bwd<4, 4, 8, 3, 4, 4>(x1, x2, g, gx1, gx2, B, C, H, W, s, ep);
     default: return hipErrorInvalidValue;
   }
 }
-constexpr int kBwdCandidates = 4;
+constexpr int kBwdCandidates = 5;
+
+// Small grids take the 4-image ring: at most this many (tile, direction, sample)
+// units. There every workgroup's channel loop is short (2-6 stages), and with
+// three stages in flight behind the g slice the loop is one load round trip
+// instead of a round trip per stage. Two runs at batch 16
+// (profiles/ab_r04/corr_bwd_ring.json, warm / cold us): L0 19.0 -> 13.9 / 24.9
+// -> 18.7, L1 18.7 -> 13.6 / 24.0 -> 17.2, L2 28.8 -> 25.4 / 32.9 -> 30.0,
+// config 1 18.7 -> 14.4, config 2 41.1 -> 40.4. From L3 up (512 units and more)
+// the ring's 60 KB cost a resident workgroup per CU: L3 38.9 -> 43.7, L4 74 -> 88.
+#ifndef USF_BWD_RING_UNITS
+#define USF_BWD_RING_UNITS 256
+#endif
 
 template <int D>
 hipError_t bwd_dispatch(const float* x1, const float* x2, const float* g, float* gx1, float* gx2,
@@ -1386,6 +1439,9 @@ hipError_t bwd_dispatch(const float* x1, const float* x2, const float* g, float*
     const int forced = variant_override(1);
     if (forced >= 0) return bwd_candidate_d4(forced, x1, x2, g, gx1, gx2, B, C, H, W, s, ep);
   }
+  using T = BwdCfg<D, 4, 8, 3, 4, 1>;  // the default tile (32 x 8)
+  const long units = (long)((W + T::TW - 1) / T::TW) * ((H + T::TH - 1) / T::TH) * B * ((gx1 && gx2) ? 2 : 1);
+  if (units <= USF_BWD_RING_UNITS) return launch_bwd<D, 4, 8, 3, 4, 4>(x1, x2, g, gx1, gx2, B, C, H, W, s, ep);
   return launch_bwd<D>(x1, x2, g, gx1, gx2, B, C, H, W, s, ep);
 }
 
