@@ -134,13 +134,14 @@ int main(int argc, char** argv) {
          pct(dur, .9), pct(dur, 1));
   printf("  max resident waves per CU %d, per SIMD %d\n", max_res(per_cu), max_res(per_simd));
   // fwd: [1] prologue DMA issue, then per stage: loop, DMA wait, barrier + next DMA issue, compute
-  // bwd: [1] prologue DMA + g slice issue, [2] -, then per stage: DMA wait, barrier + next DMA
-  //      issue, compute, barrier, combine (the combine of stage s is the next stage's first phase)
+  // bwd: [1] prologue DMA + g slice (USF_TRACE waits for the g loads), [2] stage-0 wait, then
+  //      per stage: barrier (after the previous combine), DMA issue, compute, wait for the
+  //      next stage, barrier
   const int first = fwd ? 2 : 3, stride = fwd ? 4 : 5;
   printf("  prologue (median us):");
   for (int k = 1; k < first; ++k) printf(" [%d] %.2f", k, pct(ph[k], .5));
   printf("\n  per stage (median us) %s:\n",
-         fwd ? "loop/wait/bar+issue/compute" : "wait/bar+issue/compute/bar/combine");
+         fwd ? "loop/wait/bar+issue/compute" : "combine+bar/issue/compute/wait/bar");
   for (int st = 0; first + stride * st + stride - 1 < S - 1 && !ph[first + stride * st].empty(); ++st) {
     printf("    stage %2d:", st);
     for (int k = 0; k < stride; ++k) printf(" %6.2f", pct(ph[first + stride * st + k], .5));

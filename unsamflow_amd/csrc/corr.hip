@@ -1247,22 +1247,42 @@ __device__ __forceinline__ void corr_bwd_tile(float* sm, const float* __restrict
   bwd_load_g<D, PX, SEGX, NW, CC, V, G2, AM>(gv, g + (size_t)b * ep.g_bstride, ep, b, wave, y, xb, H, W);
   USF_TRACE_VMWAIT();
   USF_TRACE_AT(1);
-  // ring: stage st in slot st % NB. Each iteration waits for stage st, then
-  // (after the barrier: every wave is done with stage st - 1's slot and the
-  // previous combine's partials) refills that slot with stage st + NB - 1.
+  // ring: stage st in slot st % NB. The first barrier waits for stage 0 only;
+  // then each iteration refills the slot of stage st - 1 (every wave is past
+  // the barrier that follows its last read of it) with stage st + NB - 1 and
+  // sums stage st. Two placements of the wait for the next stage, each the
+  // faster one where it is used (profiles/ab_r04/corr_bwd_ring.json):
+  //  * NB == 2: after the FMAs, BEFORE the combine. vmcnt also counts the
+  //    combine's global stores (gfx9 has no separate store counter), and a wait
+  //    placed after them puts their write latency on every stage (in the step
+  //    L3 49 -> 57 us, L4 73 -> 76 us);
+  //  * NB == 4 (small grids, 2-6 stages): at the top of the next iteration,
+  //    after the combine (L0/L1 16.0 -> 13.9 / 15.6 -> 13.6 us replayed).
+  // (The NB == 4 loop keeps stage 0's wait inside the loop: peeled in front of
+  // it, the same sequence measured 2 us slower at L1, profiles/ab_r04/corr_bwd_ring.json.)
+  constexpr bool TOPWAIT = NB > 2;
+  if constexpr (!TOPWAIT) {
+    if (USF_BWD_EARLY) bwd_wait_stages<F, 0, DYW * K>(wave);
+    else dma_wait_all();
+    USF_TRACE_AT(2);
+    __syncthreads();  // stage 0 landed
+  }
   int rd = 0, wr = NB - 1;
   for (int st = 0; st < nst; ++st) {
-    USF_TRACE_AT(2 + 5 * st);
-    if (st == 0 && USF_BWD_EARLY) {
-      if (NB == 2 || nst >= NB - 1) bwd_wait_stages<F, NB - 2, DYW * K>(wave);
-      else dma_wait_all();
-    } else if (NB > 2 && st + NB - 2 < nst) {
-      bwd_wait_stages<F, NB - 2, 0>(wave);
-    } else {
-      dma_wait_all();
+    if constexpr (TOPWAIT) {
+      // stage st; the stages issued after it (st + 1 .. st + NB - 2) and, at st = 0,
+      // the g slice may stay in flight
+      if (st == 0 && USF_BWD_EARLY) {
+        if (nst >= NB - 1) bwd_wait_stages<F, NB - 2, DYW * K>(wave);
+        else dma_wait_all();
+      } else if (st + NB - 2 < nst) {
+        bwd_wait_stages<F, NB - 2, 0>(wave);
+      } else {
+        dma_wait_all();
+      }
+      __syncthreads();  // stage st landed; partial slices free
     }
     USF_TRACE_AT(3 + 5 * st);
-    __syncthreads();  // stage st landed; partial slices free
     if (st + NB - 1 < nst) dma_stage(cbeg + (st + NB - 1) * CC, sm + wr * XIMG);
     const float* cur = sm + rd * XIMG;
     rd = rd + 1 == NB ? 0 : rd + 1;
@@ -1270,9 +1290,12 @@ __device__ __forceinline__ void corr_bwd_tile(float* sm, const float* __restrict
     USF_TRACE_AT(4 + 5 * st);
     bwd_stage<D, PX, SEGX, NW, CC, V, G2>(gv, cur, red + wave * (CC * TH * TW) + lane * PX, wave, r, q, ep);
     USF_TRACE_AT(5 + 5 * st);
-    __syncthreads();  // partials complete
+    if (!TOPWAIT) dma_wait_all();  // stage st + 1 (NB == 2: nothing else in flight)
     USF_TRACE_AT(6 + 5 * st);
+    __syncthreads();  // partials complete (NB == 2: and stage st + 1 landed)
+    USF_TRACE_AT(7 + 5 * st);
     bwd_combine<D, PX, SEGX, NW, CC, V>(red, gxb, tid, NT, cbeg + st * CC, cend, y0, x0, H, W, cf, fc, pow2);
+    if (!TOPWAIT && st + 1 < nst) __syncthreads();  // partial slices free for the next stage
   }
 }
 
