@@ -313,9 +313,8 @@ int usf_stream_copy_f32(const float* src, float* dst, long long n, void* stream)
  * slices per workgroup, 4 = gather for |flow| < 2 px + scatter for the rest,
  * 5 = scatter over vertically adjacent pixel pairs, 6 = the binned gather
  * (needs the workspace), 7 = the small-image kernel where H*W <= 256), op 3 = photometric
- * loss kernel (0 = row-streaming strips on producer / consumer wave pairs,
- * the default; 1 = the workgroup-tile kernel of ABI 5; 2 = row-streaming
- * strips on one wave each; 1 and 2 kept for A/B timing); index -1 restores the built-in choice. Returns the number of
+ * loss kernel (one variant: 0 = row-streaming strips on producer / consumer wave
+ * pairs; the tile and one-wave strip kernels were removed); index -1 restores the built-in choice. Returns the number of
  * variants of `op` (so index range is [0, n)), or USF_EINVAL for an unknown op
  * or out-of-range index. Process-wide; set it before launching, not
  * concurrently with launches. */

@@ -278,6 +278,11 @@ __device__ __forceinline__ TapB make_tap_b(float u, float v, int x, int y, int H
 // stream the same strip rows (the two directions, or two neighbouring strips),
 // so they take the same number of steps and barriers.
 constexpr int kRing = 4;
+// producer/consumer pairs per workgroup (A/B knob: 1 = each pair synchronises alone)
+#ifndef USF_PHOTO_PAIRS
+#define USF_PHOTO_PAIRS 2
+#endif
+constexpr int kPairs = USF_PHOTO_PAIRS;
 
 template <bool BORDER, bool GRAD, int C>
 struct PairCommon {
@@ -488,19 +493,19 @@ __device__ __forceinline__ float wave_sum(float v) {
 }
 
 template <bool BORDER, bool GRAD, int C>
-__global__ __launch_bounds__(256) void photo_pc_kernel(StripArgs a, float* __restrict__ partials) {
-  __shared__ float lds[2][2][kRing * C * 2 * 64];  // [pair][x,y | gradient state]
+__global__ __launch_bounds__(128 * kPairs) void photo_pc_kernel(StripArgs a, float* __restrict__ partials) {
+  __shared__ float lds[kPairs][2][kRing * C * 2 * 64];  // [pair][x,y | gradient state]
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int pair = wave >> 1;
   const bool prod = (wave & 1) == 0;
   // workgroup -> (sample, strip row, pair of strip items sharing that row)
-  const int npx = a.ndir == 2 ? a.nsx : (a.nsx + 1) / 2;  // workgroups per strip row
+  const int npx = kPairs == 1 ? a.ndir * a.nsx : a.ndir == 2 ? a.nsx : (a.nsx + 1) / 2;  // workgroups per strip row
   const int g = xcd_remap(blockIdx.x, gridDim.x);
   const int gx = g % npx, rest = g / npx;
   const int sy = rest % a.nsy, b = rest / a.nsy;
-  const int dirn = a.ndir == 2 ? pair : 0;
-  const int sx = a.ndir == 2 ? gx : 2 * gx + pair;
+  const int dirn = kPairs == 1 ? gx % a.ndir : a.ndir == 2 ? pair : 0;
+  const int sx = kPairs == 1 ? gx / a.ndir : a.ndir == 2 ? gx : 2 * gx + pair;
   const bool valid = sx < a.nsx;  // wave-uniform
   const int H = a.H, W = a.W;
   const int y0 = (int)((long long)sy * H / a.nsy);
@@ -637,11 +642,11 @@ StripPlan strip_plan(int B, int H, int W, int ndir) {
 template <bool BORDER, bool GRAD>
 hipError_t pc_launch_c(const StripArgs& sa, int C, dim3 grid, float* partials, hipStream_t s) {
   if (C == 3)
-    hipLaunchKernelGGL((photo_pc_kernel<BORDER, GRAD, 3>), grid, dim3(256), 0, s, sa, partials);
+    hipLaunchKernelGGL((photo_pc_kernel<BORDER, GRAD, 3>), grid, dim3(128 * kPairs), 0, s, sa, partials);
   else if (C == 2)
-    hipLaunchKernelGGL((photo_pc_kernel<BORDER, GRAD, 2>), grid, dim3(256), 0, s, sa, partials);
+    hipLaunchKernelGGL((photo_pc_kernel<BORDER, GRAD, 2>), grid, dim3(128 * kPairs), 0, s, sa, partials);
   else
-    hipLaunchKernelGGL((photo_pc_kernel<BORDER, GRAD, 1>), grid, dim3(256), 0, s, sa, partials);
+    hipLaunchKernelGGL((photo_pc_kernel<BORDER, GRAD, 1>), grid, dim3(128 * kPairs), 0, s, sa, partials);
   return hipGetLastError();
 }
 
@@ -663,7 +668,7 @@ hipError_t photo_launch(const PhotoArgs& a, int ndir, int pad_mode, float* parti
   sa.nitems = ndir * a.B * sa.nsx * sa.nsy;
   const bool grad = a.dir[0].basis != nullptr;
   // a producer / consumer pair of waves per strip, two strips per workgroup
-  const int npx = ndir == 2 ? sa.nsx : (sa.nsx + 1) / 2;
+  const int npx = kPairs == 1 ? ndir * sa.nsx : ndir == 2 ? sa.nsx : (sa.nsx + 1) / 2;
   const dim3 grid((unsigned)(a.B * sa.nsy * npx));
   hipError_t e;
   if (pad_mode == 1)
