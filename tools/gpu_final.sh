@@ -1,7 +1,9 @@
 #!/bin/bash
 # Round evidence on the GPU box: -m gpu tests, smoke, PMC traffic passes (FETCH/WRITE) -> profiles/<TAG>_pmc_traffic.json
 # (read by bench.py's roofline.traffic), the bench line, and the rocprofv3 per-site stats + roofline check.
-# Usage: TAG=r04_v2 bash tools/gpu_final.sh   (run from the repo root; outputs under gpurun_out/)
+# Usage: TAG=r04_v3 bash tools/gpu_final.sh   (run from the repo root; outputs under gpurun_out/;
+# afterwards copy gpurun_out/<TAG>_pmc_traffic.json, bench.json, prof/run_kernel_stats.csv and
+# roofline_check.json into profiles/ -- only gpurun_out/ comes back from the box)
 set -o pipefail
 R=$(pwd); TAG=${TAG:-rNN}
 mkdir -p gpurun_out

@@ -274,13 +274,17 @@ __device__ __forceinline__ TapB make_tap_b(float u, float v, int x, int y, int H
 // turns them into row sums, windows (SSIM and its coefficients) and the S
 // basis, one row behind. One workgroup barrier per step: the producer writes
 // row t while the consumer reads rows t-1 (new) and t-3 (the pixel row whose
-// basis completes), so a ring of 4 rows suffices. Both pairs of a workgroup
-// stream the same strip rows (the two directions, or two neighbouring strips),
-// so they take the same number of steps and barriers.
+// basis completes), so a ring of 4 rows suffices. With two pairs per
+// workgroup (USF_PHOTO_PAIRS=2) both stream the same strip rows (the two
+// directions, or two neighbouring strips), so they take the same number of
+// steps and barriers.
 constexpr int kRing = 4;
-// producer/consumer pairs per workgroup (A/B knob: 1 = each pair synchronises alone)
+// producer/consumer pairs per workgroup. One: each pair's barrier waits for its
+// own two waves only. Two pairs per 256-thread workgroup (round 3) kept both
+// pairs in step; one pair measured 0.3-1.3 us faster at every loss scale
+// (profiles/ab_r04/photo_pairs_per_wg.json; USF_PHOTO_PAIRS=2 for A/B).
 #ifndef USF_PHOTO_PAIRS
-#define USF_PHOTO_PAIRS 2
+#define USF_PHOTO_PAIRS 1
 #endif
 constexpr int kPairs = USF_PHOTO_PAIRS;
 
