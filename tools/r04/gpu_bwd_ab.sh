@@ -3,9 +3,12 @@
 # alternating, two runs each
 set -o pipefail
 mkdir -p gpurun_out/bab
-AB=${AB:-unsamflow_amd/lib/ab/lib_v1.so}
-timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_parity.py tests/test_gpu_corr_cat.py > gpurun_out/bab/tests.log 2>&1 || { tail -30 gpurun_out/bab/tests.log; exit 1; }
-tail -1 gpurun_out/bab/tests.log
+AB=${AB:-unsamflow_amd/lib/ab/lib_cv2.so}
+for L in main ab; do
+  if [ $L = main ]; then unset USF_LIB; else export USF_LIB=$AB; fi
+  timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_parity.py tests/test_gpu_corr_cat.py > gpurun_out/bab/tests_$L.log 2>&1 || { tail -30 gpurun_out/bab/tests_$L.log; exit 1; }
+  tail -1 gpurun_out/bab/tests_$L.log
+done
 for i in 1 2; do
   for L in main ab; do
     if [ $L = main ]; then unset USF_LIB; else export USF_LIB=$AB; fi

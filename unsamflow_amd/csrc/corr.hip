@@ -979,9 +979,6 @@ struct BwdCfg {
   static_assert(V == 1 || L::X4, "16-byte DMA needs the 4-aligned layout");
 };
 
-// One (tile, channel group) of gx1 (G2 == false: from g and x2) or gx2
-// (G2 == true: from g and x1; mirrored indices).
-
 // 1: the backward's stage-0 x DMA goes out before the g slice and the first
 // barrier waits only for it (corr_bwd_tile); 0: both waited for (vmcnt(0)).
 #ifndef USF_BWD_EARLY
@@ -1185,8 +1182,6 @@ __device__ __forceinline__ void bwd_combine(const float* red, float* gxb, int t1
   }
 }
 
-// One (tile, channel group) of gx1 (G2 == false: from g and x2) or gx2
-// (G2 == true: from g and x1; mirrored indices).
 // Wait until at most KS stages of this wave's x DMA plus EXTRA younger loads
 // are outstanding. A wave owns the J-th chunk slot of the image or not
 // (StageImg::load), so it issues one of two per-stage counts.
@@ -1198,6 +1193,8 @@ __device__ __forceinline__ void bwd_wait_stages(int wave) {
   else dma_wait_le<KS * CC * (J - 1) + EXTRA>();
 }
 
+// One (tile, channel group) of gx1 (G2 == false: from g and x2) or gx2
+// (G2 == true: from g and x1; mirrored indices).
 template <int D, int PX, int SEGX, int NW, int CC, int V, bool G2, bool AM, int NB>
 __device__ __forceinline__ void corr_bwd_tile(float* sm, const float* __restrict__ xs,
                                               const float* __restrict__ g,
@@ -1258,24 +1255,19 @@ __device__ __forceinline__ void corr_bwd_tile(float* sm, const float* __restrict
   //    L3 49 -> 57 us, L4 73 -> 76 us);
   //  * NB == 4 (small grids, 2-6 stages): at the top of the next iteration,
   //    after the combine (L0/L1 16.0 -> 13.9 / 15.6 -> 13.6 us replayed).
-  // (The NB == 4 loop keeps stage 0's wait inside the loop: peeled in front of
-  // it, the same sequence measured 2 us slower at L1, profiles/ab_r04/corr_bwd_ring.json.)
+  // (Stage 0's wait stays inside the loop: peeled in front of it, the same
+  // sequence measured 2 us slower at L1 with NB == 4 and spilled a register with NB == 2.)
   constexpr bool TOPWAIT = NB > 2;
-  if constexpr (!TOPWAIT) {
-    if (USF_BWD_EARLY) bwd_wait_stages<F, 0, DYW * K>(wave);
-    else dma_wait_all();
-    USF_TRACE_AT(2);
-    __syncthreads();  // stage 0 landed
-  }
-  int rd = 0, wr = NB - 1;
   for (int st = 0; st < nst; ++st) {
-    if constexpr (TOPWAIT) {
+    // ring slots of the stage read and of the one refilled (NB is 2 or 4: masks)
+    const int rd = st % NB, wr = (st + NB - 1) % NB;
+    if (TOPWAIT || st == 0) {
       // stage st; the stages issued after it (st + 1 .. st + NB - 2) and, at st = 0,
       // the g slice may stay in flight
       if (st == 0 && USF_BWD_EARLY) {
-        if (nst >= NB - 1) bwd_wait_stages<F, NB - 2, DYW * K>(wave);
+        if (NB == 2 || nst >= NB - 1) bwd_wait_stages<F, NB - 2, DYW * K>(wave);
         else dma_wait_all();
-      } else if (st + NB - 2 < nst) {
+      } else if (TOPWAIT && st + NB - 2 < nst) {
         bwd_wait_stages<F, NB - 2, 0>(wave);
       } else {
         dma_wait_all();
@@ -1285,8 +1277,6 @@ __device__ __forceinline__ void corr_bwd_tile(float* sm, const float* __restrict
     USF_TRACE_AT(3 + 5 * st);
     if (st + NB - 1 < nst) dma_stage(cbeg + (st + NB - 1) * CC, sm + wr * XIMG);
     const float* cur = sm + rd * XIMG;
-    rd = rd + 1 == NB ? 0 : rd + 1;
-    wr = wr + 1 == NB ? 0 : wr + 1;
     USF_TRACE_AT(4 + 5 * st);
     bwd_stage<D, PX, SEGX, NW, CC, V, G2>(gv, cur, red + wave * (CC * TH * TW) + lane * PX, wave, r, q, ep);
     USF_TRACE_AT(5 + 5 * st);
@@ -1295,7 +1285,7 @@ __device__ __forceinline__ void corr_bwd_tile(float* sm, const float* __restrict
     __syncthreads();  // partials complete (NB == 2: and stage st + 1 landed)
     USF_TRACE_AT(7 + 5 * st);
     bwd_combine<D, PX, SEGX, NW, CC, V>(red, gxb, tid, NT, cbeg + st * CC, cend, y0, x0, H, W, cf, fc, pow2);
-    if (!TOPWAIT && st + 1 < nst) __syncthreads();  // partial slices free for the next stage
+    if (!TOPWAIT) __syncthreads();  // partial slices free for the next stage
   }
 }
 
