@@ -1255,13 +1255,21 @@ __device__ __forceinline__ void corr_bwd_tile(float* sm, const float* __restrict
   //    L3 49 -> 57 us, L4 73 -> 76 us);
   //  * NB == 4 (small grids, 2-6 stages): at the top of the next iteration,
   //    after the combine (L0/L1 16.0 -> 13.9 / 15.6 -> 13.6 us replayed).
-  // (Stage 0's wait stays inside the loop: peeled in front of it, the same
-  // sequence measured 2 us slower at L1 with NB == 4 and spilled a register with NB == 2.)
+  // Stage 0's wait is peeled in front of the loop for the 16-byte-DMA two-image
+  // loop (L3/L4: 74.2 -> 72.4 us, same-box A/B) and stays inside it otherwise:
+  // peeled, NB == 4 measured 2 us slower at L1 and the dword-DMA two-image
+  // instantiation spilled a register.
   constexpr bool TOPWAIT = NB > 2;
+  constexpr bool PEEL = !TOPWAIT && V == 4;
+  if constexpr (PEEL) {
+    if (USF_BWD_EARLY) bwd_wait_stages<F, 0, DYW * K>(wave);
+    else dma_wait_all();
+    __syncthreads();  // stage 0 landed
+  }
   for (int st = 0; st < nst; ++st) {
     // ring slots of the stage read and of the one refilled (NB is 2 or 4: masks)
     const int rd = st % NB, wr = (st + NB - 1) % NB;
-    if (TOPWAIT || st == 0) {
+    if (!PEEL && (TOPWAIT || st == 0)) {
       // stage st; the stages issued after it (st + 1 .. st + NB - 2) and, at st = 0,
       // the g slice may stay in flight
       if (st == 0 && USF_BWD_EARLY) {
