@@ -164,9 +164,6 @@ __global__ __launch_bounds__(256) void photo_bwd_kernel(const float* __restrict_
 //                    complete its gradient basis.
 // Each staged pixel is warped once; the halo is 2 rows above and below each
 // strip (R chosen per shape, strip_plan) and 2 columns either side.
-#ifndef USF_PHOTO_WAVES
-#define USF_PHOTO_WAVES 2  // strips (wave pairs) per SIMD at the pair kernel's 111 VGPRs
-#endif
 constexpr int kSL = 64;        // lanes of a strip = staged columns
 constexpr int kSO = kSL - 4;   // own columns per strip (lanes 2 .. 61)
 constexpr int kOffNone = 0x7FFFFFF0;  // buffer offset past num_records: reads 0
@@ -283,6 +280,11 @@ constexpr int kRing = 4;
 // own two waves only. Two pairs per 256-thread workgroup (round 3) kept both
 // pairs in step; one pair measured 0.3-1.3 us faster at every loss scale
 // (profiles/ab_r04/photo_pairs_per_wg.json; USF_PHOTO_PAIRS=2 for A/B).
+// Occupancy target of the pair kernel, waves per SIMD (A/B knob). 4: 111
+// VGPRs with the gradient basis at C = 3, no spills.
+#ifndef USF_PHOTO_EU
+#define USF_PHOTO_EU 4
+#endif
 #ifndef USF_PHOTO_PAIRS
 #define USF_PHOTO_PAIRS 1
 #endif
@@ -497,7 +499,7 @@ __device__ __forceinline__ float wave_sum(float v) {
 }
 
 template <bool BORDER, bool GRAD, int C>
-__global__ __launch_bounds__(128 * kPairs) void photo_pc_kernel(StripArgs a, float* __restrict__ partials) {
+__global__ __launch_bounds__(128 * kPairs) __attribute__((amdgpu_waves_per_eu(USF_PHOTO_EU))) void photo_pc_kernel(StripArgs a, float* __restrict__ partials) {
   __shared__ float lds[kPairs][2][kRing * C * 2 * 64];  // [pair][x,y | gradient state]
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -607,14 +609,15 @@ __global__ __launch_bounds__(128 * kPairs) void photo_pc_kernel(StripArgs a, flo
 }
 
 // Strip heights. Every wave streams R + 4 rows, so a launch takes about
-// (R + 4) steps times the rounds of strips the chip holds: USF_PHOTO_WAVES per
-// SIMD (the pair kernel's registers), 1024 SIMDs. A step of a wave alone on its
+// (R + 4) steps times the rounds of strips the chip holds: USF_PHOTO_EU / 2
+// wave pairs per SIMD (the pair kernel's registers), 1024 SIMDs. A step of a wave alone on its
 // SIMD takes ~0.76 of a step with a second wave beside it (measured,
 // profiles/r03_photo_rows.json), so below one wave per SIMD fewer, taller
 // strips do not help. The strips of a column are balanced (heights differ by
 // at most one row); the cheapest count wins, ties to fewer strips.
 constexpr int kSimds = 1024;  // 256 CUs x 4 SIMDs
 constexpr int kMinStripRows = 4;  // the partials buffer holds ceil(H / 4) strips per column
+constexpr long long kPairSlots = (long long)USF_PHOTO_EU * kSimds / 2;  // resident strips
 
 struct StripPlan {
   int R, nsy;
@@ -633,7 +636,7 @@ StripPlan strip_plan(int B, int H, int W, int ndir) {
     const int R = (H + nsy - 1) / nsy;
     if ((H + R - 1) / R != nsy) continue;  // the same R as a smaller count
     const long long waves = cols * nsy;
-    const long long rounds = (waves + (long long)USF_PHOTO_WAVES * kSimds - 1) / ((long long)USF_PHOTO_WAVES * kSimds);
+    const long long rounds = (waves + kPairSlots - 1) / kPairSlots;
     const double cost = (double)rounds * (R + 4) * (waves > kSimds ? 1.0 : 0.76);
     if (best_cost < 0 || cost < best_cost) {
       best_cost = cost;
