@@ -1,5 +1,5 @@
 #!/bin/bash
-# correlation backward default at all seven sites: this tree's library vs an A/B build (USF_LIB),
+# correlation default (OP=bwd|fwd) at all seven sites: this tree's library vs an A/B build (USF_LIB),
 # alternating, two runs each
 set -o pipefail
 mkdir -p gpurun_out/bab
@@ -12,7 +12,7 @@ done
 for i in 1 2; do
   for L in main ab; do
     if [ $L = main ]; then unset USF_LIB; else export USF_LIB=$AB; fi
-    timeout -k 10 300 python -u tools/corrsweep.py --op bwd --variants=-1 --out gpurun_out/bab/${L}$i.json > gpurun_out/bab/${L}$i.log 2>&1 || { tail -20 gpurun_out/bab/${L}$i.log; exit 1; }
+    timeout -k 10 300 python -u tools/corrsweep.py --op ${OP:-bwd} --variants=-1 --out gpurun_out/bab/${L}$i.json > gpurun_out/bab/${L}$i.log 2>&1 || { tail -20 gpurun_out/bab/${L}$i.log; exit 1; }
   done
 done
 unset USF_LIB
