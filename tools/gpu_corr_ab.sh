@@ -1,5 +1,5 @@
 #!/bin/bash
-# correlation default (OP=bwd|fwd) at all seven sites: this tree's library vs an A/B build (USF_LIB),
+# tools/gpu_corr_ab.sh: correlation default (OP=bwd|fwd) at all seven sites: this tree's library vs an A/B build (USF_LIB),
 # alternating, two runs each
 set -o pipefail
 mkdir -p gpurun_out/bab

@@ -1,5 +1,5 @@
 #!/bin/bash
-# photometric pair: this tree's library vs an A/B build (AB=path), parity of both, then
+# tools/gpu_photo_ab.sh: photometric pair: this tree's library vs an A/B build (AB=path), parity of both, then
 # tools/photoab.py alternating, two runs each
 set -o pipefail
 mkdir -p gpurun_out/pab
