@@ -84,16 +84,17 @@ def test_sign_mask_derivative_equals_dense_pass(hip_device, B, C, H, W):
     assert torch.equal(n1, a1) and torch.equal(n2, a2)
 
 
-@pytest.mark.parametrize("B,C,H,W", [(16, 32, 64, 208), (16, 32, 112, 256), (16, 64, 32, 104)])
+@pytest.mark.parametrize("B,C,H,W", [(16, 32, 64, 208), (16, 32, 112, 256), (16, 64, 32, 104), (16, 96, 16, 52),
+                                     (16, 128, 8, 26), (16, 192, 4, 13)])
 def test_production_backward_site_vs_oracle(hip_device, B, C, H, W):
     """The decoder's backward call exactly as the step makes it (corr_cat:
     usf_corr_bwd_ex_f32 with the forward's sign mask, both gradients in one
     launch, gradient read from the concat gradient's slice) at the batch-16
-    L4 shapes -- KITTI 64x208 and Sintel 112x256 -- and KITTI L3, against the
-    fp64 oracle (correlation_native.py:13-23 autograd, restated in
-    oracle.corr) with the LeakyReLU derivative taken from the activated output
-    as the in-place module does (pwclite.py:307-308). Tolerance: atol = rtol =
-    1e-5 (the corr contract)."""
+    L4 shapes -- KITTI 64x208 and Sintel 112x256 -- and KITTI L3-L0 (L2-L0:
+    the four-image ring), against the fp64 oracle (correlation_native.py:13-23
+    autograd, restated in oracle.corr) with the LeakyReLU derivative taken from
+    the activated output as the in-place module does (pwclite.py:307-308).
+    Tolerance: atol = rtol = 1e-5 (the corr contract)."""
     from oracle.corr import corr_backward_torch64
     from unsamflow_amd import ops
 
@@ -101,7 +102,7 @@ def test_production_backward_site_vs_oracle(hip_device, B, C, H, W):
     x2 = torch.from_numpy(hashrng.normal((B, C, H, W), 402)).to(hip_device)
     buf = torch.zeros((B, 81 + C + 2, H, W), device=hip_device)
     mask = ops.corr_act_mask(B, H, W, 4, hip_device, C=C)
-    assert mask is not None  # these levels carry the sign mask in production
+    assert mask is not None  # every level carries the sign mask in production
     ops.corr_forward_ex(x1, x2, 4, buf[:, :81], 0.1, act_mask=mask)
     g = torch.from_numpy(hashrng.normal((B, 81 + C + 2, H, W), 403)).to(hip_device)
     gx1, gx2 = ops.corr_backward_ex(x1, x2, g[:, :81], 4, True, True, act_out=buf[:, :81], leaky_slope=0.1,
