@@ -69,7 +69,8 @@ def parse():
     ap.add_argument("--batch", type=int, default=8, help="pairs per GPU (kitti_base.json train.batch_size)")
     ap.add_argument("--config", choices=sorted(CONFIGS), default="kitti")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-steps", type=int, default=3)
+    ap.add_argument("--cpu-steps", type=int, default=10,
+                    help="timed CPU steps (each timed on its own: the spread is reported)")
     ap.add_argument("--cpu-batch", type=int, default=8,
                     help="CPU baseline batch: the GPU's per-rank B=8 (BASELINE.md 3)")
     ap.add_argument("--no-replay", action="store_true",
@@ -333,10 +334,17 @@ def cpu_baseline(args, cfg_name):
                      occ_backward_fn=oracle_occu_mask_backward, fused_adam=False)
     img1, img2, s1, s2 = synthetic_pair(args.cpu_batch, c["H"], c["W"], "cpu", with_seg=cfg_name != "kitti")
     step(img1, img2, s1, s2)  # warmup
-    t0 = time.perf_counter()
+    per = []
     for _ in range(args.cpu_steps):
+        t0 = time.perf_counter()
         step(img1, img2, s1, s2)
-    dt = time.perf_counter() - t0
+        per.append(time.perf_counter() - t0)
+    dt = sum(per)
+    rates = sorted(args.cpu_batch / t for t in per)
+    mean = sum(rates) / len(rates)
+    spread = {"steps": len(rates), "min": round(rates[0], 4), "median": round(rates[len(rates) // 2], 4),
+              "max": round(rates[-1], 4),
+              "std": round((sum((r - mean) ** 2 for r in rates) / max(1, len(rates) - 1)) ** 0.5, 4)}
     model = ""
     try:
         with open("/proc/cpuinfo") as f:
@@ -346,12 +354,14 @@ def cpu_baseline(args, cfg_name):
     configs = survey_configs_cpu()
     return {
         "value": round(args.cpu_batch * args.cpu_steps / dt, 4),
+        "per_step_pairs_per_s": spread,
         "survey_configs": configs,
         "corr_levels": corr_levels_cpu(),
         "unit": "image-pairs/s",
         "cores": cores,
         "kind": "port",
-        "sample": f"{args.cpu_steps} steps x B={args.cpu_batch} ({c['W']}x{c['H']}) of the same train step on CPU "
+        "sample": f"{args.cpu_steps} steps (each timed; spread in per_step_pairs_per_s) x B={args.cpu_batch} "
+                  f"({c['W']}x{c['H']}) of the same train step on CPU "
                   f"with the oracle restatement (oracle/torch_ref.py) for corr+warp+occlusion, after 1 warmup step; "
                   f"{dt:.1f} s; {model}",
     }

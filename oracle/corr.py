@@ -73,6 +73,19 @@ def corr_backward_torch64(x1: torch.Tensor, x2: torch.Tensor, g: torch.Tensor, d
     return gx1, gx2p[:, :, d:d + H, d:d + W]
 
 
+def corr_forward_torch64(x1: torch.Tensor, x2: torch.Tensor, d: int = 4) -> torch.Tensor:
+    """corr_forward_np in torch-CPU float64 (correlation_native.py:13-23, multi-threaded):
+    the checker for full-size forwards, e.g. the decoder's L4 site at batch 16."""
+    B, C, H, W = x1.shape
+    K = 2 * d + 1
+    a = x1.double()
+    x2p = F.pad(x2.double(), [d] * 4)
+    out = torch.empty((B, K * K, H, W), dtype=torch.float64)
+    for k, i, j in _shifts(d):
+        out[:, k] = (a * x2p[:, :, i:i + H, j:j + W]).mean(dim=1)
+    return out
+
+
 def corr_forward_torch(x1: torch.Tensor, x2: torch.Tensor, d: int = 4) -> torch.Tensor:
     """torch-CPU restatement of correlation_native.py:13-23 (differentiable by autograd)."""
     B, C, H, W = x1.shape

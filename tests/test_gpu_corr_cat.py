@@ -113,3 +113,70 @@ def test_production_backward_site_vs_oracle(hip_device, B, C, H, W):
     torch.testing.assert_close(gx1.cpu().double(), r1, atol=1e-5, rtol=1e-5)
     torch.testing.assert_close(gx2.cpu().double(), r2, atol=1e-5, rtol=1e-5)
 
+
+
+@pytest.mark.parametrize("B,C,H,W", [(16, 32, 64, 208), (12, 32, 40, 100), (12, 16, 40, 98), (20, 32, 24, 76)])
+def test_production_forward_site_vs_oracle(hip_device, B, C, H, W):
+    """The decoder's forward call as the step makes it (usf_corr_fwd_ex_f32: the
+    LeakyReLU epilogue into a concat slice plus the sign mask) on grids where the
+    edge-last block order of corr_fwd_kernel is active (>= USF_FWD_EDGE_MIN = 512
+    workgroups and W % 32 != 0): KITTI L4 at batch 16 (896 workgroups, the
+    production site) and three ragged grids of 540-720 workgroups on the other
+    tile configuration, 16-byte and dword staging. Every activated value against
+    the fp64 oracle (correlation_native.py:13-23, leaky_relu as pwclite.py:308),
+    atol = rtol = 1e-5; every mask bit equals (activated output > 0), and equals
+    the oracle's sign wherever |oracle| > 1e-5."""
+    from oracle.corr import corr_forward_torch64
+    from unsamflow_amd import _lib, ops
+
+    lib = _lib.load()
+    assert lib.usf_set_variant(0, -1) > 0  # the shape heuristic, not a forced candidate
+    x1 = torch.from_numpy(hashrng.normal((B, C, H, W), 501)).to(hip_device)
+    x2 = torch.from_numpy(hashrng.normal((B, C, H, W), 502)).to(hip_device)
+    buf = torch.full((B, 81 + C + 2, H, W), float("nan"), device=hip_device)
+    mask = ops.corr_act_mask(B, H, W, 4, hip_device, C=C)
+    ops.corr_forward_ex(x1, x2, 4, buf[:, :81], 0.1, act_mask=mask)
+    torch.cuda.synchronize()
+    got = buf[:, :81].cpu()
+    assert torch.isnan(buf[:, 81:]).all().item(), "forward wrote outside its concat slice"
+    ref = corr_forward_torch64(x1.cpu(), x2.cpu(), 4)
+    want = torch.where(ref > 0, ref, ref * 0.1)
+    torch.testing.assert_close(got.double(), want, atol=1e-5, rtol=1e-5)
+    W4 = (W + 3) // 4
+    bits = torch.arange(4).view(1, 1, 1, 1, 1, 4) + 4 * torch.arange(9).view(1, 1, 9, 1, 1, 1)
+    words = mask.cpu().view(B, 9, 1, H, W4, 1)
+    mbit = ((words >> bits) & 1).bool().reshape(B, 9, 9, H, 4 * W4)[..., :W]
+    mbit = mbit.reshape(B, 81, H, W)
+    assert torch.equal(mbit, got > 0)
+    clear = ref.abs() > 1e-5
+    assert torch.equal(mbit[clear], (ref > 0)[clear])
+
+
+@pytest.mark.parametrize("masked", [False, True])
+def test_backward_ring_dword_steady_state_vs_oracle(hip_device, masked):
+    """The four-image ring's steady-state wait (bwd_wait_stages<F, NB-2, 0>, reached
+    only with >= 4 stages per workgroup) on the dword-DMA path, whose per-wave
+    chunk counts differ by wave (advisor r04): (16, 192, 16, 50) is 128 units
+    (ring), 4 channel groups of 48 channels = 12 stages, W % 4 = 2 (dword DMA).
+    Plain backward and the decoder's masked form, against the fp64 oracle
+    (correlation_cuda_kernel.cu:116-300 via oracle.corr), atol = rtol = 1e-5."""
+    from oracle.corr import corr_backward_torch64
+    from unsamflow_amd import ops
+
+    B, C, H, W = 16, 192, 16, 50
+    x1 = torch.from_numpy(hashrng.normal((B, C, H, W), 601)).to(hip_device)
+    x2 = torch.from_numpy(hashrng.normal((B, C, H, W), 602)).to(hip_device)
+    g = torch.from_numpy(hashrng.normal((B, 81, H, W), 603)).to(hip_device)
+    if masked:
+        buf = torch.zeros((B, 81, H, W), device=hip_device)
+        mask = ops.corr_act_mask(B, H, W, 4, hip_device, C=C)
+        ops.corr_forward_ex(x1, x2, 4, buf, 0.1, act_mask=mask)
+        gx1, gx2 = ops.corr_backward_ex(x1, x2, g, 4, True, True, leaky_slope=0.1, act_mask=mask)
+        act = buf.cpu()
+        g_ref = torch.where(act > 0, g.cpu(), g.cpu() * 0.1)
+    else:
+        gx1, gx2 = ops.corr_backward(x1, x2, g, 4)
+        g_ref = g.cpu()
+    r1, r2 = corr_backward_torch64(x1.cpu(), x2.cpu(), g_ref, 4)
+    torch.testing.assert_close(gx1.cpu().double(), r1, atol=1e-5, rtol=1e-5)
+    torch.testing.assert_close(gx2.cpu().double(), r2, atol=1e-5, rtol=1e-5)

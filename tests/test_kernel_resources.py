@@ -48,3 +48,40 @@ def test_large_level_forward_occupancy(corr_resources):
     assert fwd, "large-level forward instantiation missing"
     for name, vgpr, _, _ in fwd:
         assert vgpr <= 72, (name, vgpr)
+
+
+def _hazard_tool():
+    import sys
+
+    sys.path.insert(0, str(REPO / "tools"))
+    import lds_dma_hazard
+
+    return lds_dma_hazard
+
+
+def test_every_lds_dma_in_the_built_library_is_guarded():
+    """every buffer_load_dword{,x4} ... lds of the library's
+    gfx950 code objects sits behind s_nop >= 4 (or 5 straight-line wait states
+    with no VALU write of an SGPR it reads) -- the hazard that faulted a box in
+    round 4 is caught here, at build time."""
+    from unsamflow_amd.build import LIB_PATH, build_library
+
+    build_library()
+    n, bad = _hazard_tool().check_library(LIB_PATH)
+    assert n > 1000, f"expected the correlation kernels' LDS-DMA sites, found {n}"
+    assert not bad, bad[:5]
+
+
+def test_lds_dma_hazard_checker_flags_an_unpadded_dma():
+    t = _hazard_tool()
+    dma = (0x20, "buffer_load_dwordx4", "v8, s[16:19], 0 offen lds")
+    unpadded = [(0x10, "v_readlane_b32", "s17, v40, 3"), (0x18, "s_mov_b32", "m0, s0"), dma]
+    padded = unpadded[:2] + [(0x1C, "s_nop", "4"), dma]
+    far = [(0x0, "v_readfirstlane_b32", "s16, v1")] + [(0x4 + 4 * i, "s_add_u32", "s2, s2, 1") for i in range(5)] \
+        + [(0x20, dma[1], dma[2])]
+    assert t.analyze(unpadded)[1] and not t.analyze(padded)[1] and not t.analyze(far)[1]
+    # a branch landing between the SGPR write and the DMA voids the straight-line argument
+    branchy = [(0x0, "v_readfirstlane_b32", "s16, v1"), (0x4, "s_cbranch_scc1", "2"), (0x8, "s_nop", "0"),
+               (0xC, "s_nop", "0"), (0x10, "s_add_u32", "s2, s2, 1"), (0x14, "s_add_u32", "s2, s2, 1"),
+               (0x18, dma[1], dma[2])]
+    assert t.analyze(branchy)[1]

@@ -43,8 +43,10 @@ def selected_sites():
 
 def main():
     lib = _lib.load()
-    if os.environ.get("USF_PHOTO_VARIANT"):  # photometric kernel A/B (usf_set_variant op 3)
-        lib.usf_set_variant(3, int(os.environ["USF_PHOTO_VARIANT"]))
+    if os.environ.get("USF_PHOTO_VARIANT"):  # usf_set_variant op 3: one pair kernel, only -1 / 0 accepted
+        v = int(os.environ["USF_PHOTO_VARIANT"])
+        if lib.usf_set_variant(3, v) < 0:
+            sys.exit(f"usf_set_variant(3, {v}) refused: no such photometric variant")
     dev = torch.device("cuda:0")
     n = int(os.environ.get("KPROF_N", "3"))
     # calibration: a plain 256 MiB device copy (16-B loads/stores) for FETCH/WRITE_SIZE scaling

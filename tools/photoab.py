@@ -21,12 +21,16 @@ from unsamflow_amd.kernel_timer import device_time_us, site_launcher  # noqa: E4
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", required=True)
-    ap.add_argument("--variant", type=int, default=-1, help="usf_set_variant(3, v): 0 strip, 1 tile kernel")
+    ap.add_argument("--variant", type=int, default=-1,
+                    help="usf_set_variant(3, v): -1 the default; the library has one pair kernel "
+                         "(producer/consumer), so any other value is refused")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     from unsamflow_amd import _lib
 
-    _lib.load().usf_set_variant(3, a.variant)
+    rc = _lib.load().usf_set_variant(3, a.variant)
+    if rc < 0:
+        sys.exit(f"usf_set_variant(3, {a.variant}) refused (rc {rc}): no such photometric variant")
     sites = [("photo_pair_grad", (8, 3, 256 >> i, 832 >> i, "border")) for i in range(4)]
     sites += [("photo_pair_grad", (8, 3, 256, 832, "zeros")), ("photo_pair", (8, 3, 256, 832, "border"))]
     rows = []

@@ -315,6 +315,9 @@ struct FwdCfg {
 #ifndef USF_FWD_EDGE_LAST
 #define USF_FWD_EDGE_LAST 1
 #endif
+#ifndef USF_FWD_EDGE_XCD
+#define USF_FWD_EDGE_XCD 1
+#endif
 #ifndef USF_FWD_EDGE_CHUNK
 #define USF_FWD_EDGE_CHUNK 8
 #endif
@@ -355,10 +358,19 @@ __global__ __launch_bounds__(64 * NDY * CS) void corr_fwd_kernel(const float* __
     // (xcd_chunk keeps dispatch order at chunk granularity): when the grid is a
     // little over one resident round (KITTI L4 at batch 16: 896 workgroups for
     // 768 slots, 128 of them edge tiles), the second round is the cheap one.
-    const int u = xcd_chunk(linear_block(), nitems, USF_FWD_EDGE_CHUNK);
-    const int g = u % F::NDYG, pi = u / F::NDYG;
     const int tf = tiles_y * (tiles_x - 1);     // full-column tiles per (sample, group)
     const int nfull = (int)(gridDim.z) * tf;
+    // Within each phase every XCD takes one contiguous run of items (xcd_remap):
+    // vertically neighbouring tiles, whose x2 halo rows overlap by 8 of 16, then
+    // share an L2. Round 4 dealt 8-item chunks round-robin instead, which put
+    // those neighbours on different XCDs: PMC fetch 57.6 -> 87.4 MB per L4
+    // launch (1.03x -> 1.26x of algorithmic). USF_FWD_EDGE_XCD=0
+    // restores the chunked deal (tools/ab_build.py).
+    const int lin = linear_block(), nf = nfull * F::NDYG;
+    const int u = !USF_FWD_EDGE_XCD ? xcd_chunk(lin, nitems, USF_FWD_EDGE_CHUNK)
+                  : lin < nf        ? xcd_remap(lin, nf)
+                                    : nf + xcd_remap(lin - nf, nitems - nf);
+    const int g = u % F::NDYG, pi = u / F::NDYG;
     int tx, ty;
     if (pi < nfull) {
       bz = pi / tf;
@@ -1085,6 +1097,20 @@ __device__ __forceinline__ void bwd_load_g(float (&gv)[DYW][K][PX], const float*
   }
 }
 
+// VMEM instructions bwd_load_g issues per wave, after the stage DMAs that the
+// backward's first wait counts past (bwd_wait_stages' EXTRA): per displacement
+// row its sign-mask words (AM: 1 for gx1, 3 for gx2) and one load per (dx,
+// 4-pixel run) on the 16-byte path, per (dx, pixel) on the dword path. Every
+// one is a separate buffer load at a runtime offset, so none can be merged.
+// The first wait leaves at most this many younger loads outstanding; a smaller
+// count would let the FMAs read a partly landed stage 0 (advisor r04).
+template <int D, int PX, int V, bool G2, bool AM, int DYW>
+constexpr int bwd_g_loads() {
+  constexpr int K = 2 * D + 1;
+  constexpr int per_dx = (USF_BWD_VECG && V == 4 && PX % 4 == 0) ? PX / 4 : PX;
+  return DYW * ((AM ? (G2 ? 3 : 1) : 0) + K * per_dx);
+}
+
 // One stage of CC channels for one wave: its DYW displacement rows summed in
 // registers per channel, the partial written lane-linear (lane*PX:
 // conflict-free ds_write_b128) to rp + c * TH * TW.
@@ -1261,8 +1287,11 @@ __device__ __forceinline__ void corr_bwd_tile(float* sm, const float* __restrict
   // instantiation spilled a register.
   constexpr bool TOPWAIT = NB > 2;
   constexpr bool PEEL = !TOPWAIT && V == 4;
+  // the first wait's EXTRA: the g slice loads issued after the stage DMAs (a lower bound)
+  constexpr int GL = DYW * K;
+  static_assert(GL <= bwd_g_loads<D, PX, V, G2, AM, DYW>(), "first wait counts past more loads than bwd_load_g issues");
   if constexpr (PEEL) {
-    if (USF_BWD_EARLY) bwd_wait_stages<F, 0, DYW * K>(wave);
+    if (USF_BWD_EARLY) bwd_wait_stages<F, 0, GL>(wave);
     else dma_wait_all();
     __syncthreads();  // stage 0 landed
   }
@@ -1273,7 +1302,7 @@ __device__ __forceinline__ void corr_bwd_tile(float* sm, const float* __restrict
       // stage st; the stages issued after it (st + 1 .. st + NB - 2) and, at st = 0,
       // the g slice may stay in flight
       if (st == 0 && USF_BWD_EARLY) {
-        if (NB == 2 || nst >= NB - 1) bwd_wait_stages<F, NB - 2, DYW * K>(wave);
+        if (NB == 2 || nst >= NB - 1) bwd_wait_stages<F, NB - 2, GL>(wave);
         else dma_wait_all();
       } else if (TOPWAIT && st + NB - 2 < nst) {
         bwd_wait_stages<F, NB - 2, 0>(wave);

@@ -58,9 +58,6 @@ __device__ __forceinline__ void warp_block(int& bx, int& b) {
 #ifndef USF_WARP_FWD_PAIR
 #define USF_WARP_FWD_PAIR 1  // forward L4 23.9 -> 13.1 us, L2 11.8 -> 7.5 us (profiles/ab_r04/warp_corner_pairs.json)
 #endif
-#ifndef USF_WARP_BWD_PAIR
-#define USF_WARP_BWD_PAIR 0
-#endif
 constexpr int kWarpOffNone = 0x7FFFFFF0;  // buffer offset past num_records: reads 0
 
 // A corner row's two taps are neighbours in memory, so each row is ONE 8-byte
@@ -414,11 +411,9 @@ __global__ __launch_bounds__(256) void warp_bwd_kernel(const float* __restrict__
     const float* xb = x + (size_t)b * C * HW;
     const float* gb = gout + (size_t)b * C * HW + (valid ? p : 0);
     float* gxb = WANT_GX ? gx + (size_t)b * C * HW : nullptr;
-    // corner pairs (pair_tap) measured no faster here (L4 56.9 vs 54.5 us,
-    // profiles/ab_r04/warp_corner_pairs.json): the filing pass is not gather-bound
-    const bool pairs = USF_WARP_BWD_PAIR && W >= 2;
-    const PairTap q = pair_tap(tp, W);
-    const auto rsx = sample_rsrc(xb, 4 * C * HW);
+    // (corner-pair loads as in the forward measured no faster here: L4 56.9 vs
+    // 54.5 us, profiles/ab_r04/warp_corner_pairs.json; the filing pass is not
+    // gather-bound, so the build-time option was removed in round 5)
 #pragma unroll 2
     for (int c = slice; c < C; c += CS) {
       const float go = valid ? gb[(size_t)c * HW] : 0.f;
@@ -428,16 +423,11 @@ __global__ __launch_bounds__(256) void warp_bwd_kernel(const float* __restrict__
         scatter_row(gc, tp.o_sw, tp.o_se, tp.m_sw, tp.m_se, go * wsw, go * wse, rs);
       }
       if (WANT_GF && valid) {
-        float vnw, vne, vsw, vse;
-        if (pairs) {
-          pair_corners(rsx, q, tp, 4u * (unsigned)(c * HW), vnw, vne, vsw, vse);
-        } else {
-          const float* xc = xb + (size_t)c * HW;
-          vnw = tp.m_nw ? xc[tp.o_nw] : 0.f;
-          vne = tp.m_ne ? xc[tp.o_ne] : 0.f;
-          vsw = tp.m_sw ? xc[tp.o_sw] : 0.f;
-          vse = tp.m_se ? xc[tp.o_se] : 0.f;
-        }
+        const float* xc = xb + (size_t)c * HW;
+        const float vnw = tp.m_nw ? xc[tp.o_nw] : 0.f;
+        const float vne = tp.m_ne ? xc[tp.o_ne] : 0.f;
+        const float vsw = tp.m_sw ? xc[tp.o_sw] : 0.f;
+        const float vse = tp.m_se ? xc[tp.o_se] : 0.f;
         dix += ((vne - vnw) * tp.s + (vse - vsw) * tp.n) * go;
         diy += ((vsw - vnw) * tp.e + (vse - vne) * tp.w) * go;
       }
