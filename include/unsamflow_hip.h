@@ -18,12 +18,13 @@
  *   usf_warp_fwd_f32  <- grid_sample(bilinear, align_corners=True) inside
  *                        flow_warp (utils/warp_utils.py:97-106, incl.
  *                        mesh_grid :7-13 and norm_grid :16-23)
- *   usf_warp_bwd_f32 / usf_warp_bwd_ex_f32
+ *   usf_warp_bwd_f32 / usf_warp_bwd_ex_f32 / usf_warp_bwd_persist_f32
  *                     <- grid_sampler_2d_backward reached from flow_warp's
  *                        autograd graph (warp_utils.py:103-105)
  *   usf_splat_map_f32 <- get_corresponding_map (warp_utils.py:26-94,
  *                        scatter_add_ of bilinear weights)
- *   usf_occ_backward_f32 <- get_occu_mask_backward (warp_utils.py:120-126),
+ *   usf_occ_backward_f32 / usf_occ_backward_persist_f32
+ *                     <- get_occu_mask_backward (warp_utils.py:120-126),
  *                        caller losses/flow_loss.py:101-103 (occ_from_back)
  *   usf_occ_bidirection_f32 <- get_occu_mask_bidirection (warp_utils.py:109-117),
  *                        caller losses/flow_loss.py:104-107 (occ_from_back = false)
@@ -46,8 +47,10 @@
  *     (losses/flow_loss.py:130-131) need no copy.
  *   - The caller allocates every output; the library never allocates,
  *     never keeps a pointer after return and has no global state except a
- *     thread-local error string and the usf_set_variant tuning override. Calls are reentrant (the backward runs on the
- *     autograd engine's device thread).
+ *     thread-local error string and the usf_set_variant tuning override.
+ *     Calls are reentrant (the backward runs on the autograd engine's device
+ *     thread). The *_persist_* entries keep state in a CALLER-owned workspace
+ *     from one call to the next (see each).
  *   - Calls are asynchronous on `stream` (a hipStream_t; NULL = legacy
  *     default stream).
  *   - Return value: 0 on success; a positive hipError_t from a failed
@@ -65,7 +68,7 @@
 extern "C" {
 #endif
 
-#define USF_ABI_VERSION 6
+#define USF_ABI_VERSION 7
 #define USF_EINVAL (-1)
 #define USF_EDEVICE (-2) /* a kernel raised a device error flag (USF_SYNC_CHECK=1 only) */
 
@@ -185,6 +188,25 @@ int usf_warp_bwd_ex_f32(const float* x, const float* flow, long long flow_bstrid
 /* Workspace bytes usf_warp_bwd_ex_f32 uses for the binned gather. */
 long long usf_warp_bwd_workspace(int B, int H, int W);
 
+/* usf_warp_bwd_ex_f32's binned gather in TWO launches (ABI 7): no per-call
+ * zero fill and no overflow pass. workspace: usf_warp_bwd_persist_workspace
+ * (B,C,H,W) bytes, 16-byte aligned, ZERO when first passed (one hipMemset at
+ * allocation). It is then reserved for calls of this (B, C, H, W) on one
+ * stream at a time; every call leaves it in a state the next call uses as is
+ * (a parity word selects one of two cell-count buffers; the gather zeroes
+ * the other), also under HIP graph replay. Pixels beyond 4 per cell are
+ * scattered (fp32 atomics, summation order not fixed) into a dense overflow
+ * buffer inside the workspace that the gather adds to its fixed-order sums
+ * and re-zeroes. gx may be NULL (then no workspace is touched); C <= 256.
+ * Results equal usf_warp_bwd_ex_f32's. */
+int usf_warp_bwd_persist_f32(const float* x, const float* flow, long long flow_bstride,
+                             const float* gout, float* gx, float* gflow, void* workspace,
+                             long long workspace_bytes, int B, int C, int H, int W, int pad_mode,
+                             void* stream);
+
+/* Workspace bytes of usf_warp_bwd_persist_f32 (0 for invalid dimensions). */
+long long usf_warp_bwd_persist_workspace(int B, int C, int H, int W);
+
 /* Forward bilinear splat of unit mass (get_corresponding_map,
  * utils/warp_utils.py:26-94): every source pixel p lands at
  *   (x, y) = absolute ? (flow[b,0,p], flow[b,1,p]) : (px + flow[b,0,p], py + flow[b,1,p])
@@ -200,6 +222,14 @@ int usf_splat_map_f32(const float* flow, long long flow_bstride, float* map,
  * occ: [B,1,H,W] dense, overwritten. */
 int usf_occ_backward_f32(const float* flow21, long long flow_bstride, float* occ,
                          int B, int H, int W, float th, void* stream);
+
+/* usf_occ_backward_f32 in two launches (ABI 7): the splat accumulates into
+ * map, the caller's persistent [B,1,H,W] fp32 buffer (map_bytes >= 4*B*H*W),
+ * which must be ZERO when first passed; the threshold pass is its only reader
+ * and zeroes it again, so no fill runs per call (graph-replay safe). One
+ * stream at a time per map. occ: [B,1,H,W] dense, overwritten. */
+int usf_occ_backward_persist_f32(const float* flow21, long long flow_bstride, float* occ, float* map,
+                                 long long map_bytes, int B, int H, int W, float th, void* stream);
 
 /* Forward-backward consistency occlusion mask (get_occu_mask_bidirection,
  * utils/warp_utils.py:109-117; stage-1 configs, occ_from_back = false), fused:

@@ -34,7 +34,8 @@ def test_header_declares_the_abi():
          "usf_corr_fwd_ex_f32", "usf_corr_fwd_workspace", "usf_corr_bwd_ex_f32", "usf_corr_act_mask_words",
          "usf_corr_bwd_ex_scratch",
          "usf_warp_fwd_f32", "usf_warp_bwd_f32", "usf_warp_bwd_ex_f32", "usf_warp_bwd_workspace",
-         "usf_splat_map_f32", "usf_occ_backward_f32",
+         "usf_warp_bwd_persist_f32", "usf_warp_bwd_persist_workspace",
+         "usf_splat_map_f32", "usf_occ_backward_f32", "usf_occ_backward_persist_f32",
          "usf_occ_bidirection_f32",
          "usf_photo_loss_partials", "usf_photo_loss_fwd_f32", "usf_photo_loss_pair_fwd_f32",
          "usf_photo_loss_bwd_f32",
@@ -59,7 +60,7 @@ def test_library_exports_every_declared_symbol(lib):
 def test_abi_version(lib):
     from unsamflow_amd import _lib
 
-    assert lib.usf_abi_version() == _lib.ABI_VERSION == 6
+    assert lib.usf_abi_version() == _lib.ABI_VERSION == 7
 
 
 def test_no_torch_types_in_abi():
@@ -96,6 +97,10 @@ def test_no_torch_types_in_abi():
         (lambda L: L.usf_splat_map_f32(None, 2 * 16, 1, 1, 4, 4, 0, None), "null pointer"),
         (lambda L: L.usf_occ_backward_f32(1, 3, 1, 2, 4, 4, 0.2, None), "batch stride"),
         (lambda L: L.usf_occ_backward_f32(1, 32, None, 1, 4, 4, 0.2, None), "null pointer"),
+        (lambda L: L.usf_occ_backward_persist_f32(1, 32, 16, 16, 60, 1, 4, 4, 0.2, None), "separate buffer"),
+        (lambda L: L.usf_occ_backward_persist_f32(1, 32, 16, 16, 64, 1, 4, 4, 0.2, None), "separate buffer"),
+        (lambda L: L.usf_warp_bwd_persist_f32(1, 1, 32, 1, 1, 1, 16, 64, 1, 3, 4, 4, 1, None), "persistent workspace"),
+        (lambda L: L.usf_warp_bwd_persist_f32(1, 1, 32, 1, 1, 1, 16, 1 << 40, 1, 300, 4, 4, 1, None), "C=300"),
         (lambda L: L.usf_photo_loss_fwd_f32(1, 1, 1, 1, 32, 1, 1, None, 1, 4, 4, 4, 1, 0.15, 0.85, None), "> 3"),
         (lambda L: L.usf_photo_loss_fwd_f32(1, 1, 1, 1, 32, 1, 1, 1, 1, 3, 4, 4, 9, 0.15, 0.85, None), "pad_mode 9"),
         (lambda L: L.usf_photo_loss_fwd_f32(1, None, 1, 1, 32, 1, 1, None, 1, 3, 4, 4, 1, 0.15, 0.85, None), "null input"),
@@ -161,3 +166,14 @@ def test_warp_bwd_workspace_size(lib):
     cells = B * (H + 1) * (W + 1)
     assert 4 * cells * (1 + 4 + 16) + 4 * B * H * W <= n <= 4 * cells * (1 + 4 + 16) + 4 * B * H * W + 5 * 256
     assert lib.usf_warp_bwd_workspace(0, H, W) == 0
+
+
+def test_warp_bwd_persist_workspace_size(lib):
+    """Persistent form: two count buffers, 4 slots + weights per cell, a dirty
+    word per gather tile, a dense [B,C,H,W] overflow buffer; 0 when invalid."""
+    B, C, H, W = 16, 32, 64, 208
+    n = lib.usf_warp_bwd_persist_workspace(B, C, H, W)
+    cells = B * (H + 1) * (W + 1)
+    lo = 4 * cells * (2 + 4 + 16) + 4 * B * C * H * W
+    assert lo <= n <= lo + 4 * B * 7 * 8 + 6 * 256
+    assert lib.usf_warp_bwd_persist_workspace(B, 0, H, W) == 0

@@ -1,0 +1,120 @@
+"""The two-launch persistent forms (ABI 7):
+usf_warp_bwd_persist_f32 (binned gather without the per-call zero fill and
+the overflow pass) and usf_occ_backward_persist_f32 (splat + threshold, the
+threshold re-zeroes the splat buffer). Their workspaces carry state from one
+call to the next, so every test runs a SEQUENCE of calls on one workspace --
+overflow-heavy, then smooth, then overflow-heavy again, and a second shape in
+between -- and checks each against the per-call forms (usf_warp_bwd_ex_f32,
+usf_occ_backward_f32), which zero their state on every call:
+grad_flow bit-identical, grad_x bit-identical where no cell overflows and
+within atol 1e-5 where overflow entries are summed by fp32 atomics
+(utils/warp_utils.py:97-106 / :120-126 via the reference-pinned per-call forms).
+"""
+import pytest
+import torch
+
+from unsamflow_amd import _lib, ops
+
+pytestmark = pytest.mark.gpu
+
+
+def _fields(B, H, W, dev):
+    yy = torch.arange(H, device=dev, dtype=torch.float32).view(1, H, 1).expand(1, H, W)
+    xx = torch.arange(W, device=dev, dtype=torch.float32).view(1, 1, W).expand(1, H, W)
+    smooth = torch.cat([1.7 * torch.sin(xx / 9.0) + 0.3, 1.2 * torch.cos(yy / 7.0) - 0.4]).expand(B, 2, H, W)
+    shift = smooth.clone()
+    shift[:, 0] += W / 8.0  # border-clamped strip: many sources on one edge cell per row (overflow)
+    contract = torch.cat([0.9 * ((W - 1) / 2.0 - xx), 0.9 * ((H - 1) / 2.0 - yy)]).expand(B, 2, H, W)
+    return {"smooth": smooth.contiguous(), "shift": shift.contiguous(), "contract": contract.contiguous()}
+
+
+def _ex(x, flow, go, pad):
+    """usf_warp_bwd_ex_f32: the four-launch form with a fresh workspace (zero-filled by the call)."""
+    lib = _lib.load()
+    B, C, H, W = x.shape
+    gx, gf = torch.empty_like(x), torch.empty(B, 2, H, W, device=x.device)
+    n = int(lib.usf_warp_bwd_workspace(B, H, W))
+    ws = torch.empty(n, device=x.device, dtype=torch.uint8)
+    rc = lib.usf_warp_bwd_ex_f32(x.data_ptr(), flow.data_ptr(), 2 * H * W, go.data_ptr(), gx.data_ptr(),
+                                 gf.data_ptr(), ws.data_ptr(), n, B, C, H, W,
+                                 _lib.PAD_BORDER if pad == "border" else _lib.PAD_ZEROS,
+                                 _lib.stream_handle(x.device))
+    _lib.check(rc, "usf_warp_bwd_ex_f32")
+    return gx, gf
+
+
+@pytest.mark.parametrize("pad", ["border", "zeros"])
+def test_warp_persist_call_sequence_matches_per_call_form(hip_device, pad):
+    shapes = [(4, 32, 64, 208), (3, 16, 33, 70)]
+    data = {}
+    for i, (B, C, H, W) in enumerate(shapes):
+        g = torch.Generator(device=hip_device).manual_seed(20 + i)
+        data[(B, C, H, W)] = (torch.randn(B, C, H, W, device=hip_device, generator=g),
+                              torch.randn(B, C, H, W, device=hip_device, generator=g),
+                              _fields(B, H, W, hip_device))
+    seq = [(0, "shift"), (0, "smooth"), (1, "contract"), (0, "contract"), (0, "smooth"), (1, "smooth"),
+           (0, "shift"), (1, "shift"), (0, "smooth")]
+    for si, kind in seq:
+        x, go, fields = data[shapes[si]]
+        flow = fields[kind]
+        gx, gf = ops.warp_backward(x, flow, go, pad, True, True)  # the persistent form
+        rx, rf = _ex(x, flow, go, pad)
+        assert torch.equal(gf, rf), (shapes[si], kind)
+        if kind == "smooth":
+            assert torch.equal(gx, rx), (shapes[si], kind)  # no overflow: the same fixed-order sums
+        else:
+            torch.testing.assert_close(gx, rx, atol=1e-5, rtol=1e-5, msg=lambda m: f"{shapes[si]} {kind}: {m}")
+
+
+def test_warp_persist_workspace_returns_to_reusable_state(hip_device):
+    """After an overflow-heavy call and a smooth one, the workspace holds no
+    leftover: the overflow buffer and every dirty word are zero again, and one
+    of the two count buffers is zero (the one the next call files into)."""
+    B, C, H, W = 2, 16, 40, 64
+    g = torch.Generator(device=hip_device).manual_seed(31)
+    x = torch.randn(B, C, H, W, device=hip_device, generator=g)
+    go = torch.randn(B, C, H, W, device=hip_device, generator=g)
+    f = _fields(B, H, W, hip_device)
+    ops.warp_backward(x, f["contract"], go, "border")
+    ops.warp_backward(x, f["smooth"], go, "border")
+    torch.cuda.synchronize()
+    ws = ops.persistent_workspace(hip_device, "warp_bwd", (B, C, H, W), 0)
+    # layout of warp.hip bin_layout2, restated: header, 2 count buffers, slots, weights, dirty words, overflow
+    al = lambda v: (v + 255) & ~255  # noqa: E731
+    cells = B * (H + 1) * (W + 1)
+    ntiles = ((W + 31) // 32) * ((H + 7) // 8)
+    bins_off = al(256 + 8 * cells)
+    dirty_off = al(al(bins_off + 16 * cells) + 64 * cells)
+    total = al(al(dirty_off + 4 * B * ntiles) + 4 * B * C * H * W)
+    assert total == int(_lib.load().usf_warp_bwd_persist_workspace(B, C, H, W)) <= ws.numel()
+    assert int(torch.count_nonzero(ws[dirty_off:total])) == 0  # dirty words and the overflow buffer
+    hdr = ws[:8].view(torch.int32).cpu()
+    cnt = ws[256:256 + 8 * cells].view(torch.int32).view(2, cells)
+    nxt = int(hdr[0])
+    assert nxt in (0, 1) and int(torch.count_nonzero(cnt[nxt])) == 0
+
+
+def test_occ_persist_call_sequence_matches_per_call_form(hip_device):
+    lib = _lib.load()
+    for B, H, W in [(8, 256, 832), (2, 40, 64), (8, 256, 832)]:
+        f = _fields(B, H, W, hip_device)
+        for kind in ("smooth", "contract", "shift", "smooth"):
+            flow = f[kind]
+            got = ops.occ_backward(flow, 0.2)  # the persistent form
+            ref = torch.empty_like(got)
+            rc = lib.usf_occ_backward_f32(flow.data_ptr(), 2 * H * W, ref.data_ptr(), B, H, W, 0.2,
+                                          _lib.stream_handle(hip_device))
+            _lib.check(rc, "usf_occ_backward_f32")
+            # masks agree except where the splat sum sits within 1e-5 of the threshold
+            # (atomic summation order, as in tests/test_gpu_parity.py's occlusion checks)
+            diff = (got != ref)
+            if diff.any():
+                m = torch.empty_like(got)
+                rc = lib.usf_splat_map_f32(flow.data_ptr(), 2 * H * W, m.data_ptr(), B, H, W, 0,
+                                           _lib.stream_handle(hip_device))
+                _lib.check(rc, "usf_splat_map_f32")
+                assert bool(((m[diff].clamp(0, 1) - 0.2).abs() < 1e-5).all()), (B, H, W, kind)
+    torch.cuda.synchronize()
+    for key, ws in ops._PERSIST.items():
+        if key[1] == "occ_bwd":
+            assert int(torch.count_nonzero(ws)) == 0, key  # the threshold pass left every map zero

@@ -17,7 +17,7 @@ from pathlib import Path
 import torch  # noqa: F401  (load torch's HIP runtime before the plugin)
 
 _LIB_PATH = Path(os.environ.get("USF_LIB", Path(__file__).resolve().parent / "lib" / "libunsamflow_hip.so"))
-ABI_VERSION = 6
+ABI_VERSION = 7
 PAD_ZEROS = 0
 PAD_BORDER = 1
 
@@ -64,6 +64,17 @@ _SIGNATURES = {
         ctypes.c_int,
     ),
     "usf_warp_bwd_workspace": ([ctypes.c_int] * 3, ctypes.c_longlong),
+    "usf_warp_bwd_persist_f32": (
+        [_c_float_p, _c_float_p, ctypes.c_longlong, _c_float_p, _c_float_p, _c_float_p, ctypes.c_void_p,
+         ctypes.c_longlong] + [ctypes.c_int] * 5 + [ctypes.c_void_p],
+        ctypes.c_int,
+    ),
+    "usf_warp_bwd_persist_workspace": ([ctypes.c_int] * 4, ctypes.c_longlong),
+    "usf_occ_backward_persist_f32": (
+        [_c_float_p, ctypes.c_longlong, _c_float_p, _c_float_p, ctypes.c_longlong] + [ctypes.c_int] * 3
+        + [ctypes.c_float, ctypes.c_void_p],
+        ctypes.c_int,
+    ),
     "usf_splat_map_f32": (
         [_c_float_p, ctypes.c_longlong, _c_float_p] + [ctypes.c_int] * 4 + [ctypes.c_void_p],
         ctypes.c_int,

@@ -253,7 +253,7 @@ int usf_warp_fwd_f32(const float* x, const float* flow, long long flow_bstride, 
 
 static int warp_bwd_common(const char* fn, const float* x, const float* flow, long long flow_bstride,
                            const float* gout, float* gx, float* gflow, void* ws, long long ws_bytes, int B,
-                           int C, int H, int W, int pad_mode, void* stream) {
+                           int C, int H, int W, int pad_mode, void* stream, bool persist = false) {
   clear_error();
   if (!check_dims(fn, B, C, H, W)) return USF_EINVAL;
   if (pad_mode != USF_PAD_ZEROS && pad_mode != USF_PAD_BORDER) {
@@ -276,10 +276,21 @@ static int warp_bwd_common(const char* fn, const float* x, const float* flow, lo
     set_error("%s: workspace must be 16-byte aligned", fn);
     return USF_EINVAL;
   }
+  if (persist) {
+    if (!ws || ws_bytes < warp_bwd_persist_workspace(B, C, H, W)) {
+      set_error("%s: persistent workspace of %lld bytes < usf_warp_bwd_persist_workspace = %lld", fn, ws_bytes,
+                warp_bwd_persist_workspace(B, C, H, W));
+      return USF_EINVAL;
+    }
+    if (C > 256 || H >= 32768 || W >= 65536) {  // gather channel groups fit a 32-bit dirty mask; packed (y, x)
+      set_error("%s: C=%d H=%d W=%d beyond the persistent form (C <= 256, H < 32768, W < 65536)", fn, C, H, W);
+      return USF_EINVAL;
+    }
+  }
   if (const int pe = pre_check(fn, (hipStream_t)stream)) return pe;
   return finish(fn,
                 warp_bwd_launch(x, flow, flow_bstride, gout, gx, gflow, B, C, H, W, pad_mode,
-                                (hipStream_t)stream, ws, ws_bytes),
+                                (hipStream_t)stream, ws, ws_bytes, persist),
                 (hipStream_t)stream);
 }
 
@@ -300,6 +311,18 @@ int usf_warp_bwd_ex_f32(const float* x, const float* flow, long long flow_bstrid
 long long usf_warp_bwd_workspace(int B, int H, int W) {
   if (B <= 0 || H <= 0 || W <= 0) return 0;
   return warp_bwd_workspace(B, H, W);
+}
+
+int usf_warp_bwd_persist_f32(const float* x, const float* flow, long long flow_bstride, const float* gout,
+                             float* gx, float* gflow, void* workspace, long long workspace_bytes, int B, int C,
+                             int H, int W, int pad_mode, void* stream) {
+  return warp_bwd_common("usf_warp_bwd_persist_f32", x, flow, flow_bstride, gout, gx, gflow, workspace,
+                         workspace_bytes, B, C, H, W, pad_mode, stream, true);
+}
+
+long long usf_warp_bwd_persist_workspace(int B, int C, int H, int W) {
+  if (B <= 0 || C <= 0 || H <= 0 || W <= 0) return 0;
+  return warp_bwd_persist_workspace(B, C, H, W);
 }
 
 static bool check_splat(const char* fn, const float* flow, long long fbs, const float* out, int B,
@@ -333,6 +356,21 @@ int usf_occ_backward_f32(const float* flow21, long long flow_bstride, float* occ
   if (const int pe = pre_check("usf_occ_backward_f32", (hipStream_t)stream)) return pe;
   return finish("usf_occ_backward_f32",
                 occ_backward_launch(flow21, flow_bstride, occ, B, H, W, th, (hipStream_t)stream),
+                (hipStream_t)stream);
+}
+
+int usf_occ_backward_persist_f32(const float* flow21, long long flow_bstride, float* occ, float* map,
+                                 long long map_bytes, int B, int H, int W, float th, void* stream) {
+  clear_error();
+  const char* fn = "usf_occ_backward_persist_f32";
+  if (!check_splat(fn, flow21, flow_bstride, occ, B, H, W)) return USF_EINVAL;
+  if (!map || map_bytes < 4LL * B * H * W || map == occ) {
+    set_error("%s: map must be a separate buffer of >= 4*B*H*W = %lld bytes (got %lld)", fn, 4LL * B * H * W,
+              map_bytes);
+    return USF_EINVAL;
+  }
+  if (const int pe = pre_check(fn, (hipStream_t)stream)) return pe;
+  return finish(fn, occ_backward_persist_launch(flow21, flow_bstride, occ, map, B, H, W, th, (hipStream_t)stream),
                 (hipStream_t)stream);
 }
 

@@ -1356,6 +1356,9 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(USF_BWD
 #ifndef USF_BWD_DIRFAST
 #define USF_BWD_DIRFAST 0
 #endif
+#ifndef USF_BWD_GROUP_XCD
+#define USF_BWD_GROUP_XCD 1
+#endif
 #ifndef USF_BWD_DIRFAST_CHUNK
 #define USF_BWD_DIRFAST_CHUNK 28
 #endif
@@ -1374,6 +1377,13 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(USF_BWD
     // (profiles/ab_r01/bwd_chunk_*.json); whole-sample chunks (xcd_remap) are
     // slower (84 us) and so are levels with < 16 tiles (L1 11.6 -> 13.5 us).
     w = xcd_chunk(w, gridDim.x * gridDim.y * gridDim.z, dirfast ? USF_BWD_DIRFAST_CHUNK : USF_BWD_CHUNK);
+  } else if (USF_BWD_GROUP_XCD && gridDim.y > 1) {
+    // Small grids (KITTI L0-L2, the four-image ring) split a tile's channels over
+    // gridDim.y groups, each of which loads the tile's whole g slice (81 planes).
+    // In the linear order the groups of a tile are consecutive blocks, i.e. on
+    // different XCDs, so every group misses its own L2 (PMC traffic 2.7x of
+    // algorithmic at L2). One XCD chunk per tile's groups.
+    w = xcd_chunk(w, gridDim.x * gridDim.y * gridDim.z, gridDim.y);
   }
   int group, tile, b;
   if (dirfast) {

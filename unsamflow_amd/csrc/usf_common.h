@@ -101,14 +101,20 @@ hipError_t warp_fwd_launch(const float* x, const float* flow, long long flow_bst
 hipError_t warp_bwd_launch(const float* x, const float* flow, long long flow_bstride,
                            const float* gout, float* gx, float* gflow, int B, int C, int H,
                            int W, int pad_mode, hipStream_t s, void* workspace = nullptr,
-                           long long workspace_bytes = 0);
+                           long long workspace_bytes = 0, bool persist = false);
 // bytes of workspace for the binned-gather grad_x (usf_warp_bwd_ex_f32)
 long long warp_bwd_workspace(int B, int H, int W);
+// bytes of the persistent workspace of usf_warp_bwd_persist_f32
+long long warp_bwd_persist_workspace(int B, int C, int H, int W);
 
 hipError_t splat_launch(const float* flow, long long flow_bstride, float* map, int B, int H, int W,
                         bool absolute, hipStream_t s);
 hipError_t occ_backward_launch(const float* flow, long long flow_bstride, float* occ, int B, int H,
                                int W, float th, hipStream_t s);
+hipError_t splat_scatter(const float* flow, long long flow_bstride, float* map, int B, int H, int W,
+                         bool absolute, hipStream_t s);
+hipError_t occ_backward_persist_launch(const float* flow, long long flow_bstride, float* occ, float* map, int B,
+                                       int H, int W, float th, hipStream_t s);
 hipError_t occ_bidirection_launch(const float* flow12, long long bs12, const float* flow21, long long bs21,
                                   float* occ, int B, int H, int W, float scale, float bias, hipStream_t s);
 

@@ -329,6 +329,7 @@ __device__ __forceinline__ bool gather_inlier(float u, float v) {
 // cell: strongly compressive flow, or border clamping) are listed and added
 // afterwards with float atomics.
 constexpr int kBinSlots = 4;
+constexpr int kBinTW = 32, kBinTH = 8;  // target tile of the gather pass (warp_gx_bins_kernel)
 struct BinArgs {
   int* cnt = nullptr;      // [B][(H+1)(W+1)] pixels filed per cell
   int* bins = nullptr;     // [B][(H+1)(W+1)][kBinSlots] source pixel (py << 16 | px)
@@ -338,9 +339,18 @@ struct BinArgs {
   int* ovf = nullptr;      // [B * HW] overflow list: b * HW + p
   int* novf = nullptr;     // overflow list length
   int ovf_cap = 0;         // list capacity (B * HW): a pixel is listed at most once per call
+  // Persistent workspace (BIN == 2, usf_warp_bwd_persist_f32; see bwd_bins_persist):
+  // two count buffers chosen by a parity word, overflow pixels scattered into a
+  // dense [B][C][H][W] buffer that the gather adds and re-zeroes per dirty tile.
+  int* hdr = nullptr;          // [0]: parity the filing pass reads, [1]: the gather's
+  int* cnt2 = nullptr;         // 2 x [B (H+1)(W+1)] count buffers
+  float* ovfgx = nullptr;      // [B][C][H][W] overflow contributions (zero between calls)
+  unsigned* dirty = nullptr;   // [B][tiles]: bit g = channel group g of the gather has overflow to add
+  unsigned dmask = 0;          // all groups' bits
+  int tiles_x = 0, ntiles = 0; // the gather's 32 x 8 target tiles
 };
 
-template <bool BORDER, bool WANT_GX, bool WANT_GF, int CS, int OUTL = 0, bool BIN = false>
+template <bool BORDER, bool WANT_GX, bool WANT_GF, int CS, int OUTL = 0, int BIN = 0>
 __global__ __launch_bounds__(256) void warp_bwd_kernel(const float* __restrict__ x,
                                                        const float* __restrict__ flow,
                                                        long long fbs,
@@ -369,6 +379,13 @@ __global__ __launch_bounds__(256) void warp_bwd_kernel(const float* __restrict__
   }
   if (!valid) tp.m_nw = tp.m_ne = tp.m_sw = tp.m_se = false;
   if (OUTL && !__syncthreads_or(valid)) return;  // no outlier in this workgroup (uniform)
+  bool ovf = false;  // BIN == 2: p did not get a slot; its contributions go to ba.ovfgx
+  if (BIN == 2) {
+    // parity of this call's count buffer; handed to the gather (which flips it for the next call)
+    const int par = __builtin_amdgcn_readfirstlane(*(volatile const int*)ba.hdr);
+    ba.cnt = ba.cnt2 + (size_t)par * ba.ncell;
+    if (t == 0) ba.hdr[1] = par;
+  }
   if (BIN && slice == 0 && valid) {
     // file p under its north-west corner cell (see BinArgs); weights as the scatter forms them
     if (tp.m_nw || tp.m_ne || tp.m_sw || tp.m_se) {  // then xw in [-1, W), yn in [-1, H)
@@ -382,12 +399,41 @@ __global__ __launch_bounds__(256) void warp_bwd_kernel(const float* __restrict__
         wb[ks] = tp.m_ne ? tp.s * tp.w : 0.f;
         wb[2 * ks] = tp.m_sw ? tp.n * tp.e : 0.f;
         wb[3 * ks] = tp.m_se ? tp.n * tp.w : 0.f;
-      } else {
+      } else if (BIN == 1) {
         // scattered by the overflow pass; the capacity test only matters if the
         // per-call zero fill of novf / counts did not run (every pixel lists once)
         const int o = atomicAdd(ba.novf, 1);
         if (o < ba.ovf_cap) ba.ovf[o] = b * HW + p;
+      } else {
+        // persistent form: scattered below into ba.ovfgx; every gather workgroup of
+        // the target tiles its corners touch adds that buffer (and re-zeroes it)
+        ovf = true;
+        const int qy[2] = {tp.yn, tp.yn + 1}, qx[2] = {tp.xw, tp.xw + 1};
+        const bool mk[4] = {tp.m_nw, tp.m_ne, tp.m_sw, tp.m_se};
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          if (mk[k])
+            ba.dirty[(size_t)b * ba.ntiles + (qy[k >> 1] / kBinTH) * ba.tiles_x + qx[k & 1] / kBinTW] = ba.dmask;
       }
+    }
+  }
+  RowRuns ron{}, ros{};  // BIN == 2: reduce-by-key runs of the overflow pixels' corner rows
+  bool wave_ovf = false;
+  if (BIN == 2) {
+    __shared__ unsigned char ovf_s[PXB];
+    if (slice == 0) ovf_s[pl] = ovf;
+    __syncthreads();
+    ovf = ovf_s[pl] != 0;
+    wave_ovf = __any(ovf);
+    if (wave_ovf) {  // wave-uniform: every lane takes part in the shuffles
+      const int lane = t & 63;
+      const bool has_left = pl > 0 && lane != 0, has_right = pl + 1 < PXB && lane != 63;
+      const bool vx = ovf && tp.xw >= -1 && tp.xw < W;
+      const bool vyn = vx && (unsigned)tp.yn < (unsigned)H, vys = vx && (unsigned)(tp.yn + 1) < (unsigned)H;
+      ron = row_runs(vyn ? tp.yn * (W + 1) + tp.xw + 1 : -(lane + 2), ovf && tp.m_nw, ovf && tp.m_ne, has_left,
+                     has_right);
+      ros = row_runs(vys ? (tp.yn + 1) * (W + 1) + tp.xw + 1 : -(lane + 2), ovf && tp.m_sw, ovf && tp.m_se,
+                     has_left, has_right);
     }
   }
   // grad_x: reduce-by-key over the wave per corner row (see scatter_row)
@@ -421,6 +467,11 @@ __global__ __launch_bounds__(256) void warp_bwd_kernel(const float* __restrict__
         float* gc = gxb + (size_t)c * HW;
         scatter_row(gc, tp.o_nw, tp.o_ne, tp.m_nw, tp.m_ne, go * wnw, go * wne, rn);
         scatter_row(gc, tp.o_sw, tp.o_se, tp.m_sw, tp.m_se, go * wsw, go * wse, rs);
+      }
+      if (BIN == 2 && wave_ovf) {
+        float* oc = ba.ovfgx + ((size_t)b * C + c) * HW;
+        scatter_row(oc, tp.o_nw, tp.o_ne, ovf && tp.m_nw, ovf && tp.m_ne, go * wnw, go * wne, ron);
+        scatter_row(oc, tp.o_sw, tp.o_se, ovf && tp.m_sw, ovf && tp.m_se, go * wsw, go * wse, ros);
       }
       if (WANT_GF && valid) {
         const float* xc = xb + (size_t)c * HW;
@@ -471,9 +522,9 @@ __device__ __forceinline__ void cswap(int& a, int& b) {
 // per pass of kGatherCH channels when it holds at most kBoxCap pixels
 // (smooth flows: the tile shifted by the local flow, plus its spread), else
 // the sources are read from global memory directly.
-constexpr int kBinTW = 32, kBinTH = 8;
 constexpr int kBoxW = 64, kBoxH = 16;  // staged box: rows of kBoxW floats (lane = column)
 constexpr int kBoxCap = kBoxW * kBoxH;
+template <bool PERSIST = false>
 __global__ __launch_bounds__(256) void warp_gx_bins_kernel(const float* __restrict__ gout, BinArgs ba,
                                                            float* __restrict__ gx, int C, int H, int W,
                                                            int tiles_x, int cper) {
@@ -488,6 +539,18 @@ __global__ __launch_bounds__(256) void warp_gx_bins_kernel(const float* __restri
   const int c0 = blockIdx.z * cper, c1 = min(C, c0 + cper);
   const bool valid = qy < H && qx < W;
   const int qq = valid ? qy * W + qx : 0;
+  bool dirty = false;  // PERSIST: this (tile, channel group) has overflow contributions to add
+  if (PERSIST) {
+    // this call's counts (the parity the filing pass handed over); the other
+    // buffer is zeroed here for the next call, which reads the flipped parity
+    const int par = __builtin_amdgcn_readfirstlane(*(volatile const int*)(ba.hdr + 1));
+    ba.cnt = ba.cnt2 + (size_t)par * ba.ncell;
+    int* other = ba.cnt2 + (size_t)(1 - par) * ba.ncell;
+    const long long nth = (long long)gridDim.x * gridDim.y * gridDim.z * 256;
+    for (long long i = (long long)linear_block() * 256 + t; i < ba.ncell; i += nth) other[i] = 0;
+    if (t == 0) ba.hdr[0] = 1 - par;
+    dirty = (ba.dirty[(size_t)b * ba.ntiles + blockIdx.x] >> blockIdx.z) & 1u;
+  }
   if (t == 0) {
     bb[0] = INT_MAX; bb[1] = INT_MIN; bb[2] = INT_MAX; bb[3] = INT_MIN;
   }
@@ -620,12 +683,24 @@ __global__ __launch_bounds__(256) void warp_gx_bins_kernel(const float* __restri
             for (int u = 0; u < kGatherCH; ++u) acc[u] = fmaf(wk[k][j], src[co[u]], acc[u]);
           }
     }
+    if (PERSIST && dirty && valid) {
+      // the overflow pixels' contributions (scattered by the filing pass), then
+      // re-zeroed: this workgroup is their only reader
+      float* oq = ba.ovfgx + (size_t)b * C * HW + qq;
+#pragma unroll
+      for (int u = 0; u < kGatherCH; ++u)
+        if (c + u < c1) {
+          acc[u] += oq[(size_t)(c + u) * HW];
+          oq[(size_t)(c + u) * HW] = 0.f;
+        }
+    }
     if (valid) {
 #pragma unroll
       for (int u = 0; u < kGatherCH; ++u)
         if (c + u < c1) gq[(size_t)(c + u) * HW] = acc[u];
     }
   }
+  if (PERSIST && dirty && t == 0) atomicAnd(ba.dirty + (size_t)b * ba.ntiles + blockIdx.x, ~(1u << blockIdx.z));
 }
 
 // Overflow pixels of the binned grad_x add their four corner contributions
@@ -1118,16 +1193,64 @@ inline BinLayout bin_layout(int B, int H, int W) {
   return L;
 }
 
-template <bool BORDER, int CS>
+template <bool BORDER, int CS, int BINM>
 void bin_pass_cs(const float* x, const float* flow, long long fbs, const float* gout, float* gflow, int B,
                  int C, int H, int W, BinArgs ba, hipStream_t s) {
   const dim3 grid((unsigned)((H * W + 256 / CS - 1) / (256 / CS)), (unsigned)B), block(256);
   if (gflow)
-    hipLaunchKernelGGL((warp_bwd_kernel<BORDER, false, true, CS, false, true>), grid, block, 0, s, x, flow, fbs,
+    hipLaunchKernelGGL((warp_bwd_kernel<BORDER, false, true, CS, 0, BINM>), grid, block, 0, s, x, flow, fbs,
                        gout, nullptr, gflow, B, C, H, W, ba);
   else
-    hipLaunchKernelGGL((warp_bwd_kernel<BORDER, false, false, CS, false, true>), grid, block, 0, s, x, flow,
+    hipLaunchKernelGGL((warp_bwd_kernel<BORDER, false, false, CS, 0, BINM>), grid, block, 0, s, x, flow,
                        fbs, gout, nullptr, nullptr, B, C, H, W, ba);
+}
+
+// The gather pass's grid: 32 x 8 target tiles x B x channel groups (multiples
+// of kGatherCH) until ~1024 workgroups, i.e. >= 16 channels per workgroup
+// wherever the grid allows (L3: 43.3 -> 38.3 us against ~2048;
+// profiles/ab_r02/warp_bins_ab.json).
+#ifndef USF_BIN_WGS
+#define USF_BIN_WGS 1024
+#endif
+struct GatherGrid {
+  int tiles_x, ntiles, cper, zg;
+};
+inline GatherGrid gather_grid(int B, int C, int H, int W) {
+  GatherGrid g;
+  g.tiles_x = (W + kBinTW - 1) / kBinTW;
+  g.ntiles = g.tiles_x * ((H + kBinTH - 1) / kBinTH);
+  const long units = (long)g.ntiles * B;
+  const int chunks = (C + kGatherCH - 1) / kGatherCH;
+  const int want = (int)std::min<long>(chunks, std::max<long>(1, (USF_BIN_WGS + units - 1) / units));
+  g.cper = ((chunks + want - 1) / want) * kGatherCH;
+  g.zg = (C + g.cper - 1) / g.cper;
+  return g;
+}
+
+// filing pass, with grad_flow's channel slices chosen as for the scatter: the
+// smallest slice count in {4, 16, 64} that still gives >= 768 workgroups
+// (profiles/ab_r02/warp_bins_ab.json: L2 31.5 -> 26.7 us with 16 instead of 4;
+// L3/L4 keep 4, L1 64)
+template <bool BORDER, int BINM>
+void bin_pass(const float* x, const float* flow, long long fbs, const float* gout, float* gflow, int B, int C,
+              int H, int W, BinArgs ba, hipStream_t s) {
+  int cs = 64;
+  for (const int o : {4, 16}) {
+    if ((long)B * ((H * W + 256 / o - 1) / (256 / o)) >= 768) {
+      cs = o;
+      break;
+    }
+  }
+  while (cs > 4 && cs > C) cs >>= 2;  // no more slices than channels (4 at least)
+#ifdef USF_BIN_CS
+  cs = USF_BIN_CS;  // A/B builds only
+#endif
+  switch (cs) {
+    case 1: bin_pass_cs<BORDER, 1, BINM>(x, flow, fbs, gout, gflow, B, C, H, W, ba, s); break;
+    case 4: bin_pass_cs<BORDER, 4, BINM>(x, flow, fbs, gout, gflow, B, C, H, W, ba, s); break;
+    case 16: bin_pass_cs<BORDER, 16, BINM>(x, flow, fbs, gout, gflow, B, C, H, W, ba, s); break;
+    default: bin_pass_cs<BORDER, 64, BINM>(x, flow, fbs, gout, gflow, B, C, H, W, ba, s); break;
+  }
 }
 
 // grad_x by the binned gather (+ grad_flow in the filing pass); see BinArgs.
@@ -1145,44 +1268,64 @@ void bwd_bins(const float* x, const float* flow, long long fbs, const float* gou
   ba.novf = reinterpret_cast<int*>(w + L.novf_off);
   ba.ovf_cap = B * H * W;
   (void)zero_fill(w, (size_t)(L.cnt_off + 4LL * B * (H + 1) * (W + 1)), s);  // novf + counts
-  // filing pass, with grad_flow's channel slices chosen as for the scatter
-  // the smallest slice count in {4, 16, 64} that still gives >= 768 workgroups
-  // (profiles/ab_r02/warp_bins_ab.json: L2 31.5 -> 26.7 us with 16 instead of 4;
-  // L3/L4 keep 4, L1 64)
-  int cs = 64;
-  for (const int o : {4, 16}) {
-    if ((long)B * ((H * W + 256 / o - 1) / (256 / o)) >= 768) {
-      cs = o;
-      break;
-    }
-  }
-  while (cs > 4 && cs > C) cs >>= 2;  // no more slices than channels (4 at least)
-#ifdef USF_BIN_CS
-  cs = USF_BIN_CS;  // A/B builds only
-#endif
-  switch (cs) {
-    case 1: bin_pass_cs<BORDER, 1>(x, flow, fbs, gout, gflow, B, C, H, W, ba, s); break;
-    case 4: bin_pass_cs<BORDER, 4>(x, flow, fbs, gout, gflow, B, C, H, W, ba, s); break;
-    case 16: bin_pass_cs<BORDER, 16>(x, flow, fbs, gout, gflow, B, C, H, W, ba, s); break;
-    default: bin_pass_cs<BORDER, 64>(x, flow, fbs, gout, gflow, B, C, H, W, ba, s); break;
-  }
-  // gather pass: 32 x 8 target tiles, channel groups (multiples of kGatherCH)
-  // until ~2048 workgroups
-  const int tiles_x = (W + kBinTW - 1) / kBinTW, ntiles = tiles_x * ((H + kBinTH - 1) / kBinTH);
-  const long units = (long)ntiles * B;
-  const int chunks = (C + kGatherCH - 1) / kGatherCH;
-// ~1024 workgroups, i.e. >= 16 channels per workgroup wherever the grid
-// allows (L3: 43.3 -> 38.3 us against ~2048; profiles/ab_r02/warp_bins_ab.json)
-#ifndef USF_BIN_WGS
-#define USF_BIN_WGS 1024
-#endif
-  const int want = (int)std::min<long>(chunks, std::max<long>(1, (USF_BIN_WGS + units - 1) / units));
-  const int cper = ((chunks + want - 1) / want) * kGatherCH;
-  const int zg = (C + cper - 1) / cper;
-  hipLaunchKernelGGL(warp_gx_bins_kernel, dim3((unsigned)ntiles, (unsigned)B, (unsigned)zg), dim3(256), 0, s, gout,
-                     ba, gx, C, H, W, tiles_x, cper);
+  bin_pass<BORDER, 1>(x, flow, fbs, gout, gflow, B, C, H, W, ba, s);
+  const GatherGrid gg = gather_grid(B, C, H, W);
+  hipLaunchKernelGGL(warp_gx_bins_kernel<false>, dim3((unsigned)gg.ntiles, (unsigned)B, (unsigned)gg.zg), dim3(256),
+                     0, s, gout, ba, gx, C, H, W, gg.tiles_x, gg.cper);
   // overflow pixels (few or none for smooth flows): listed, scattered with atomics
   hipLaunchKernelGGL((warp_gx_ovf_kernel<BORDER>), dim3(256), dim3(256), 0, s, flow, fbs, gout, ba, gx, C, H, W);
+}
+
+// Persistent-workspace form (usf_warp_bwd_persist_f32): TWO launches, no fill
+// and no overflow pass. The workspace is zero when first handed over and is
+// left reusable: the filing pass counts into the buffer the parity word
+// selects, the gather zeroes the other one and flips the parity for the next
+// call (each word has one writer kernel and is read by the other, so launch
+// order on the stream is the only synchronisation: graph-replay safe).
+// Overflow pixels (more than kBinSlots per cell) are scattered by the filing
+// pass into a dense [B][C][H][W] buffer with the same reduce-by-key atomics as
+// the old overflow pass, and every target tile they touch is marked dirty for
+// each gather channel group; that group's workgroup adds the buffer into its
+// sums and zeroes it again (its only reader). The summation order of a cell
+// is the bins' (fixed), then the overflow sum, as in the four-launch form.
+struct BinLayout2 {
+  long long hdr_off, cnt_off, bins_off, wbin_off, dirty_off, ovfgx_off, total;
+};
+inline BinLayout2 bin_layout2(int B, int C, int H, int W) {
+  auto al = [](long long v) { return (v + 255) & ~255LL; };
+  const long long E = (long long)B * (H + 1) * (W + 1);
+  const GatherGrid gg = gather_grid(B, C, H, W);
+  BinLayout2 L;
+  L.hdr_off = 0;
+  L.cnt_off = 256;
+  L.bins_off = al(L.cnt_off + 2 * 4 * E);
+  L.wbin_off = al(L.bins_off + 4 * E * kBinSlots);
+  L.dirty_off = al(L.wbin_off + 16 * E * kBinSlots);
+  L.ovfgx_off = al(L.dirty_off + 4LL * B * gg.ntiles);
+  L.total = al(L.ovfgx_off + 4LL * B * C * H * W);
+  return L;
+}
+
+template <bool BORDER>
+void bwd_bins_persist(const float* x, const float* flow, long long fbs, const float* gout, float* gx, float* gflow,
+                      int B, int C, int H, int W, void* ws, hipStream_t s) {
+  const BinLayout2 L = bin_layout2(B, C, H, W);
+  const GatherGrid gg = gather_grid(B, C, H, W);
+  char* w = static_cast<char*>(ws);
+  BinArgs ba;
+  ba.hdr = reinterpret_cast<int*>(w + L.hdr_off);
+  ba.cnt2 = reinterpret_cast<int*>(w + L.cnt_off);
+  ba.bins = reinterpret_cast<int*>(w + L.bins_off);
+  ba.wbin = reinterpret_cast<float*>(w + L.wbin_off);
+  ba.ncell = (long long)B * (H + 1) * (W + 1);
+  ba.dirty = reinterpret_cast<unsigned*>(w + L.dirty_off);
+  ba.ovfgx = reinterpret_cast<float*>(w + L.ovfgx_off);
+  ba.dmask = gg.zg >= 32 ? ~0u : (1u << gg.zg) - 1u;
+  ba.tiles_x = gg.tiles_x;
+  ba.ntiles = gg.ntiles;
+  bin_pass<BORDER, 2>(x, flow, fbs, gout, gflow, B, C, H, W, ba, s);
+  hipLaunchKernelGGL(warp_gx_bins_kernel<true>, dim3((unsigned)gg.ntiles, (unsigned)B, (unsigned)gg.zg), dim3(256),
+                     0, s, gout, ba, gx, C, H, W, gg.tiles_x, gg.cper);
 }
 
 // --------------------------------------------------- small-image backward --
@@ -1419,7 +1562,12 @@ __global__ __launch_bounds__(kSmallNT) void warp_bwd_small_kernel(const float* _
 template <bool BORDER>
 void bwd_launch_pad(const float* x, const float* flow, long long fbs, const float* gout,
                     float* gx, float* gflow, int B, int C, int H, int W, hipStream_t s,
-                    void* ws = nullptr, long long ws_bytes = 0) {
+                    void* ws = nullptr, long long ws_bytes = 0, bool persist = false) {
+  if (persist) {  // usf_warp_bwd_persist_f32 (capi.cpp checked the workspace size and C)
+    if (gx) bwd_bins_persist<BORDER>(x, flow, fbs, gout, gx, gflow, B, C, H, W, ws, s);
+    else bwd_launch_pad<BORDER>(x, flow, fbs, gout, gx, gflow, B, C, H, W, s);  // grad_flow only: no workspace
+    return;
+  }
   // usf_set_variant(2, 2 / 3): lane-merged scatter with CS forced to 4 / 1
   // (whole-wave pixel runs) instead of the occupancy-driven choice
   const int v = variant_override(2);
@@ -1625,11 +1773,15 @@ __global__ __launch_bounds__(256) void splat_pair_kernel(const float* __restrict
   if (split) scatter_row(mb, on1, on1 + 1, s1.m_nw && own1, s1.m_ne && own1, s1.ax0 * s1.ay0, s1.ax1 * s1.ay0, r3);
 }
 
-// occ = clamp(map, 0, 1) < th ? 1 : 0, in place (get_occu_mask_backward :124-126)
-__global__ __launch_bounds__(256) void occ_threshold_kernel(float* __restrict__ m, long long n,
-                                                            float th) {
+// occ = clamp(map, 0, 1) < th ? 1 : 0 (get_occu_mask_backward :124-126); in
+// place (occ == map), or (REZERO) from a persistent map that is zeroed as read
+template <bool REZERO>
+__global__ __launch_bounds__(256) void occ_threshold_kernel(float* m, float* occ, long long n, float th) {
   const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (i < n) m[i] = fminf(fmaxf(m[i], 0.f), 1.f) < th ? 1.f : 0.f;
+  if (i >= n) return;
+  const float v = m[i];
+  if (REZERO) m[i] = 0.f;
+  occ[i] = fminf(fmaxf(v, 0.f), 1.f) < th ? 1.f : 0.f;
 }
 
 }  // namespace
@@ -1656,21 +1808,28 @@ hipError_t warp_fwd_launch(const float* x, const float* flow, long long fbs, flo
 
 hipError_t warp_bwd_launch(const float* x, const float* flow, long long fbs, const float* gout,
                            float* gx, float* gflow, int B, int C, int H, int W, int pad_mode,
-                           hipStream_t s, void* ws, long long ws_bytes) {
+                           hipStream_t s, void* ws, long long ws_bytes, bool persist) {
   if (!gx && !gflow) return hipSuccess;
   if (pad_mode == 1)
-    bwd_launch_pad<true>(x, flow, fbs, gout, gx, gflow, B, C, H, W, s, ws, ws_bytes);
+    bwd_launch_pad<true>(x, flow, fbs, gout, gx, gflow, B, C, H, W, s, ws, ws_bytes, persist);
   else
-    bwd_launch_pad<false>(x, flow, fbs, gout, gx, gflow, B, C, H, W, s, ws, ws_bytes);
+    bwd_launch_pad<false>(x, flow, fbs, gout, gx, gflow, B, C, H, W, s, ws, ws_bytes, persist);
   return hipGetLastError();
 }
 
 long long warp_bwd_workspace(int B, int H, int W) { return bin_layout(B, H, W).total; }
+long long warp_bwd_persist_workspace(int B, int C, int H, int W) { return bin_layout2(B, C, H, W).total; }
 
 hipError_t splat_launch(const float* flow, long long fbs, float* map, int B, int H, int W,
                         bool absolute, hipStream_t s) {
   hipError_t e = zero_fill(map, (size_t)B * H * W * sizeof(float), s);
   if (e != hipSuccess) return e;
+  return splat_scatter(flow, fbs, map, B, H, W, absolute, s);
+}
+
+// the splat's scatter into a map that is already zero
+hipError_t splat_scatter(const float* flow, long long fbs, float* map, int B, int H, int W, bool absolute,
+                         hipStream_t s) {
   const long pairs = (long)W * ((H + 1) / 2);
   if (pairs >= 4096 && variant_override(2) != 0) {  // pixel pairs (as the warp backward)
     const dim3 grid((unsigned)((pairs + 255) / 256), (unsigned)B);
@@ -1688,12 +1847,24 @@ hipError_t splat_launch(const float* flow, long long fbs, float* map, int B, int
   return hipGetLastError();
 }
 
+hipError_t occ_backward_persist_launch(const float* flow, long long fbs, float* occ, float* map, int B, int H,
+                                       int W, float th, hipStream_t s) {
+  // map: the caller's persistent splat buffer, zero on entry; the threshold pass
+  // is its only reader and leaves it zero again (no fill launch)
+  hipError_t e = splat_scatter(flow, fbs, map, B, H, W, false, s);
+  if (e != hipSuccess) return e;
+  const long long n = (long long)B * H * W;
+  hipLaunchKernelGGL(occ_threshold_kernel<true>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, map, occ, n,
+                     th);
+  return hipGetLastError();
+}
+
 hipError_t occ_backward_launch(const float* flow, long long fbs, float* occ, int B, int H, int W,
                                float th, hipStream_t s) {
   hipError_t e = splat_launch(flow, fbs, occ, B, H, W, false, s);
   if (e != hipSuccess) return e;
   const long long n = (long long)B * H * W;
-  hipLaunchKernelGGL(occ_threshold_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, occ, n,
+  hipLaunchKernelGGL(occ_threshold_kernel<false>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, occ, occ, n,
                      th);
   return hipGetLastError();
 }

@@ -167,6 +167,28 @@ def warp_forward(x: torch.Tensor, flow: torch.Tensor, pad: str = "border") -> to
     return out
 
 
+# Persistent workspaces of the *_persist_* entry points (include/unsamflow_hip.h,
+# ABI 7): zeroed once when created, then left reusable by every call, so the
+# per-call fill launch is gone. One per (device, op, shape). Calls of one op and
+# shape must not overlap on two streams at once: this package issues every call
+# on torch's current stream, and its graph captures (kernel_timer, harness) warm
+# up on a side stream that the capture stream waits for -- so the capture reuses
+# the eager workspace and records no fill.
+_PERSIST: dict = {}
+
+
+def persistent_workspace(device: torch.device, op: str, shape: tuple, nbytes: int) -> torch.Tensor:
+    """The zero-initialised persistent workspace of ``op`` at ``shape`` on
+    ``device`` (created on first use with torch.zeros on the current stream, so
+    the zeroing is ordered before the first call)."""
+    key = (device.index, op, shape)
+    ws = _PERSIST.get(key)
+    if ws is None or ws.numel() < nbytes:
+        ws = torch.zeros(nbytes, device=device, dtype=torch.uint8)
+        _PERSIST[key] = ws
+    return ws
+
+
 def warp_backward(
     x: torch.Tensor,
     flow: torch.Tensor,
@@ -177,13 +199,14 @@ def warp_backward(
 ) -> tuple[torch.Tensor | None, torch.Tensor | None]:
     """(grad_x, grad_flow) of :func:`warp_forward`.
 
-    grad_x is the library's binned gather (``usf_warp_bwd_ex_f32``): every
-    source pixel is filed under its north-west corner cell and each target cell
-    sums its sources in a fixed order, so grad_x is deterministic unless a cell
-    receives more than 4 source pixels (strongly compressive flow), whose
-    excess is added with fp32 atomics. The call allocates a workspace of
-    ``usf_warp_bwd_workspace(B, H, W)`` bytes (about 88 B per pixel) from
-    torch's caching allocator. grad_flow is deterministic."""
+    grad_x is the library's binned gather in its two-launch persistent form
+    (``usf_warp_bwd_persist_f32``): every source pixel is filed under its
+    north-west corner cell and each target cell sums its sources in a fixed
+    order, so grad_x is deterministic unless a cell receives more than 4 source
+    pixels (strongly compressive flow), whose excess is added with fp32
+    atomics. Its workspace (``usf_warp_bwd_persist_workspace``: ~88 B per pixel
+    plus one float per element of x) is kept per stream and shape
+    (:func:`persistent_workspace`). grad_flow is deterministic."""
     _require_device_f32("x", x)
     _require_device_f32("flow12", flow)
     _require_device_f32("grad_output", grad_out)
@@ -200,18 +223,22 @@ def warp_backward(
     gx = torch.empty_like(xc) if need_x else None  # overwritten by the library
     gf = torch.empty((B, 2, H, W), device=x.device, dtype=torch.float32) if need_flow else None
     lib = _lib.load()
-    # grad_x by the binned gather: its workspace comes from torch's caching allocator
-    nws = int(lib.usf_warp_bwd_workspace(B, H, W)) if need_x else 0
-    ws = torch.empty(nws, device=x.device, dtype=torch.uint8) if nws > 0 else None
-    with torch.cuda.device(x.device), _kt.timed(
-        "warp_bwd", (B, C, H, W, pad, need_x, need_flow), x.device,
-        _kt.warp_bytes(B, C, H, W, True, need_x, need_flow),
-    ):
-        rc = lib.usf_warp_bwd_ex_f32(
-            xc.data_ptr(), fv.data_ptr(), fbs, gc.data_ptr(), _ptr(gx), _ptr(gf), _ptr(ws), nws,
-            B, C, H, W, PAD_MODES[pad], _lib.stream_handle(x.device),
-        )
-    _lib.check(rc, "usf_warp_bwd_ex_f32")
+    # grad_x by the binned gather, persistent two-launch form (C <= 256), else the
+    # four-launch form with a per-call workspace from torch's caching allocator
+    persist = need_x and C <= 256 and H < 32768 and W < 65536
+    with torch.cuda.device(x.device):
+        if persist:
+            nws = int(lib.usf_warp_bwd_persist_workspace(B, C, H, W))
+            ws = persistent_workspace(x.device, "warp_bwd", (B, C, H, W), nws)
+        else:
+            nws = int(lib.usf_warp_bwd_workspace(B, H, W)) if need_x else 0
+            ws = torch.empty(nws, device=x.device, dtype=torch.uint8) if nws > 0 else None
+        fn = lib.usf_warp_bwd_persist_f32 if persist else lib.usf_warp_bwd_ex_f32
+        with _kt.timed("warp_bwd", (B, C, H, W, pad, need_x, need_flow), x.device,
+                       _kt.warp_bytes(B, C, H, W, True, need_x, need_flow)):
+            rc = fn(xc.data_ptr(), fv.data_ptr(), fbs, gc.data_ptr(), _ptr(gx), _ptr(gf), _ptr(ws), nws,
+                    B, C, H, W, PAD_MODES[pad], _lib.stream_handle(x.device))
+    _lib.check(rc, "usf_warp_bwd_persist_f32" if persist else "usf_warp_bwd_ex_f32")
     return gx, gf
 
 
@@ -245,11 +272,15 @@ def occ_backward(flow21: torch.Tensor, th: float = 0.2) -> torch.Tensor:
     fv, fbs, B, H, W = _flow_arg(flow21, "flow21")
     out = torch.empty((B, 1, H, W), device=flow21.device, dtype=torch.float32)
     lib = _lib.load()
-    with torch.cuda.device(flow21.device), _kt.timed("occ_bwd", (B, 1, H, W), flow21.device,
-                                                       4 * B * H * W * 3):
-        rc = lib.usf_occ_backward_f32(fv.data_ptr(), fbs, out.data_ptr(), B, H, W, float(th),
-                                      _lib.stream_handle(flow21.device))
-    _lib.check(rc, "usf_occ_backward_f32")
+    with torch.cuda.device(flow21.device):
+        # the splat map lives in a persistent zeroed buffer that the threshold pass
+        # re-zeroes (usf_occ_backward_persist_f32: two launches, no fill)
+        nmap = 4 * B * H * W
+        ws = persistent_workspace(flow21.device, "occ_bwd", (B, H, W), nmap)
+        with _kt.timed("occ_bwd", (B, 1, H, W), flow21.device, 4 * B * H * W * 3):
+            rc = lib.usf_occ_backward_persist_f32(fv.data_ptr(), fbs, out.data_ptr(), ws.data_ptr(), nmap, B, H, W,
+                                                  float(th), _lib.stream_handle(flow21.device))
+    _lib.check(rc, "usf_occ_backward_persist_f32")
     return out
 
 
