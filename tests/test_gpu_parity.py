@@ -310,7 +310,7 @@ def test_correlation_cuda_shim_reference_call_pattern(hip_device):
         correlation_cuda.forward(t1, t2, rbot1, rbot2, output, 3, 3, 20, 1, 2, 1)
 
 
-@pytest.mark.parametrize("shape", [(2, 40, 13, 37), (1, 192, 4, 13), (2, 32, 64, 70)])
+@pytest.mark.parametrize("shape", [(2, 40, 13, 37), (1, 192, 4, 13), (2, 32, 64, 70), (2, 24, 24, 64)])
 def test_corr_every_tile_variant_vs_oracle(hip_device, shape):
     """Every d=4 tile variant reachable through usf_set_variant computes the same result."""
     from unsamflow_amd import _lib, ops

@@ -26,7 +26,7 @@ timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method threa
 tail -2 $O/persist_tests.log
 timeout -k 10 600 python -u -m pytest tests -q -m gpu -x --timeout 300 --timeout-method thread > $O/pytest.log 2>&1
 rc=$?; tail -3 $O/pytest.log; [ $rc -eq 0 ] || { grep -E "^E |FAILED|Error" $O/pytest.log | head -30; exit 1; }
-timeout -k 10 300 python -u tools/persist_ab.py --out $O/persist_ab.json > $O/persist_ab.log 2>&1 || { tail -20 $O/persist_ab.log; exit 1; }
-timeout -k 10 600 python bench.py --config sintel_mf --no-cpu-baseline > $O/sintel_mf.json 2> $O/sintel_mf.err || { grep -v MIOpen $O/sintel_mf.err | tail -20; exit 1; }
-head -c 400 $O/sintel_mf.json; echo
+for i in 1 2; do
+  timeout -k 10 300 python -u tools/corrsweep.py --op bwd --variants=-1,5,6 --out $O/bwd_flags$i.json > $O/bwd_flags$i.log 2>&1 || { tail -20 $O/bwd_flags$i.log; exit 1; }
+done
 echo R05A_DONE

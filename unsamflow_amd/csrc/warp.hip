@@ -1563,14 +1563,19 @@ template <bool BORDER>
 void bwd_launch_pad(const float* x, const float* flow, long long fbs, const float* gout,
                     float* gx, float* gflow, int B, int C, int H, int W, hipStream_t s,
                     void* ws = nullptr, long long ws_bytes = 0, bool persist = false) {
-  if (persist) {  // usf_warp_bwd_persist_f32 (capi.cpp checked the workspace size and C)
-    if (gx) bwd_bins_persist<BORDER>(x, flow, fbs, gout, gx, gflow, B, C, H, W, ws, s);
-    else bwd_launch_pad<BORDER>(x, flow, fbs, gout, gx, gflow, B, C, H, W, s);  // grad_flow only: no workspace
-    return;
-  }
   // usf_set_variant(2, 2 / 3): lane-merged scatter with CS forced to 4 / 1
   // (whole-wave pixel runs) instead of the occupancy-driven choice
   const int v = variant_override(2);
+  if (persist) {  // usf_warp_bwd_persist_f32 (capi.cpp checked the workspace size and C)
+    if (gx && (v < 0 || v == 6)) {
+      bwd_bins_persist<BORDER>(x, flow, fbs, gout, gx, gflow, B, C, H, W, ws, s);
+      return;
+    }
+    // grad_flow only, or a forced variant: the per-call dispatch WITHOUT the
+    // workspace (its layout differs; the persistent state stays untouched)
+    ws = nullptr;
+    ws_bytes = 0;
+  }
   // small images (decoder level 1): one launch (usf_set_variant(2, 7) where
   // it fits; off by default, see USF_WARP_SMALL)
   if ((v == 7 || (v < 0 && USF_WARP_SMALL)) && H * W <= kSmallMaxHW && H >= 2 && W >= 2 && (gx || gflow)) {
