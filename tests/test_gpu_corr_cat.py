@@ -180,34 +180,3 @@ def test_backward_ring_dword_steady_state_vs_oracle(hip_device, masked):
     r1, r2 = corr_backward_torch64(x1.cpu(), x2.cpu(), g_ref, 4)
     torch.testing.assert_close(gx1.cpu().double(), r1, atol=1e-5, rtol=1e-5)
     torch.testing.assert_close(gx2.cpu().double(), r2, atol=1e-5, rtol=1e-5)
-
-
-@pytest.mark.parametrize("variant", [5, 6])
-@pytest.mark.parametrize("B,C,H,W", [(16, 32, 64, 208), (16, 64, 32, 104), (4, 40, 24, 70)])
-def test_barrier_free_backward_equals_default(hip_device, variant, B, C, H, W):
-    """usf_set_variant(1, 5 / 6): the backward whose stages hand over through
-    per-wave LDS step counters instead of workgroup barriers (corr_bwd_flags_kernel,
-    CC = 2 / 4) sums every channel in the same order as the default kernel, so
-    with the decoder's sign mask at the L4 / L3 sites (and a dword-staged ragged
-    shape) both gradients are BIT-identical to the default's; the default is
-    checked against the fp64 oracle by test_production_backward_site_vs_oracle."""
-    from unsamflow_amd import _lib, ops
-
-    lib = _lib.load()
-    x1 = torch.from_numpy(hashrng.normal((B, C, H, W), 801)).to(hip_device)
-    x2 = torch.from_numpy(hashrng.normal((B, C, H, W), 802)).to(hip_device)
-    buf = torch.zeros((B, 81 + C + 2, H, W), device=hip_device)
-    mask = ops.corr_act_mask(B, H, W, 4, hip_device, C=C)
-    ops.corr_forward_ex(x1, x2, 4, buf[:, :81], 0.1, act_mask=mask)
-    g = torch.from_numpy(hashrng.normal((B, 81 + C + 2, H, W), 803)).to(hip_device)
-    try:
-        lib.usf_set_variant(1, 0)
-        d1, d2 = ops.corr_backward_ex(x1, x2, g[:, :81], 4, True, True, leaky_slope=0.1, act_mask=mask)
-        lib.usf_set_variant(1, variant)
-        f1, f2 = ops.corr_backward_ex(x1, x2, g[:, :81], 4, True, True, leaky_slope=0.1, act_mask=mask)
-        o1, _ = ops.corr_backward_ex(x1, x2, g[:, :81], 4, True, False, leaky_slope=0.1, act_mask=mask)
-        _, o2 = ops.corr_backward_ex(x1, x2, g[:, :81], 4, False, True, leaky_slope=0.1, act_mask=mask)
-    finally:
-        lib.usf_set_variant(1, -1)
-    assert torch.equal(f1, d1) and torch.equal(f2, d2)
-    assert torch.equal(o1, d1) and torch.equal(o2, d2)

@@ -34,7 +34,6 @@
 //    partials are added through LDS in a fixed order and written once.
 #include <algorithm>
 #include <cstdint>
-#include <type_traits>
 
 #include "usf_common.h"
 
@@ -1411,167 +1410,6 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(USF_BWD
   }
 }
 
-// ------------------------------------------- backward without stage barriers --
-// USF_BWD_FLAGS = 1: the gather backward of
-// corr_bwd_tile with the per-stage workgroup barriers replaced by monotonic
-// per-wave step counters in LDS. Each wave waits only for what it reads:
-//  * LD[w]: wave w's share of stage s landed (its own counted vmcnt wait);
-//    the FMAs of stage s wait for all three shares;
-//  * PD[w]: wave w wrote its partials of stage s; the partials of a stage are
-//    combined one stage LATER (each wave a third), so that wait is normally
-//    already satisfied, and the x slot of stage s-1 is refilled (stage s+2)
-//    behind the same wait;
-//  * CB[w]: wave w combined its third of stage s; the partial slot of stage s
-//    is rewritten at stage s + 2.
-// Three x slots (two stages in flight) and two partial slots of CC = 2
-// channels: 30 KB, so four workgroups of three waves per CU as before. The
-// combine's stores are counted out of the x waits conservatively (a wait for
-// stage s counts only the DMA instructions issued after it: stores issued in
-// between are waited for too, never fewer than the stage).
-#ifndef USF_BWD_FLAGS
-#define USF_BWD_FLAGS 0
-#endif
-template <int D, int PX, int SEGX, int NW, int CC, int V>
-struct FlagCfg {
-  using F = BwdCfg<D, PX, SEGX, NW, CC, V>;
-  static constexpr int NS = 3, NP = 2;
-  static constexpr int RED1 = NW * CC * F::TH * F::TW;  // one partial slot
-  static constexpr int LDSN = NS * F::XIMG + NP * RED1 + 16;
-};
-
-// all of the NW counters at f reach v (one 16-byte LDS read per poll)
-template <int NW>
-__device__ __forceinline__ void flags_wait_all(const int* f, int v) {
-  static_assert(NW <= 4, "one ds_read_b128 per poll");
-  using i32x4 = int __attribute__((ext_vector_type(4)));
-  while (true) {
-    const i32x4 q = *reinterpret_cast<const volatile i32x4*>(f);
-    const int m = NW == 1 ? q.x : NW == 2 ? min(q.x, q.y) : NW == 3 ? min(min(q.x, q.y), q.z)
-                                                            : min(min(q.x, q.y), min(q.z, q.w));
-    if (m >= v) break;
-    __builtin_amdgcn_s_sleep(1);
-  }
-  asm volatile("" ::: "memory");
-}
-__device__ __forceinline__ void flag_publish(int* f, int v) {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's LDS writes (and reads) are done
-  if ((threadIdx.x & 63) == 0) __hip_atomic_store(f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-
-template <int D, int PX, int SEGX, int NW, int CC, int V, bool G2, bool AM>
-__device__ __forceinline__ void corr_bwd_tile_flags(float* sm, const float* __restrict__ xs,
-                                                    const float* __restrict__ g, float* __restrict__ gx,
-                                                    int tile, int group, int b, int C, int H, int W,
-                                                    int tiles_x, int cg, const BwdEpi& ep) {
-  using F = BwdCfg<D, PX, SEGX, NW, CC, V>;
-  using FC = FlagCfg<D, PX, SEGX, NW, CC, V>;
-  constexpr int K = F::K, TW = F::TW, TH = F::TH, DYW = F::DYW, XIMG = F::XIMG, NS = FC::NS;
-  constexpr int RED1 = FC::RED1;
-  float* red = sm + NS * XIMG;  // two partial slots
-  int* fl = reinterpret_cast<int*>(red + FC::NP * RED1);  // LD[4], PD[4], CB[4]
-  int* const LD = fl;
-  int* const PD = fl + 4;
-  int* const CB = fl + 8;
-
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int cbeg = group * cg, cend = min(C, cbeg + cg);
-  const int ty = tile / tiles_x, tx = tile - ty * tiles_x;
-  const int y0 = ty * TH, x0 = tx * TW;
-  const int r = F::L::row(lane), q = F::L::seg(lane);
-  const int y = y0 + r, xb = x0 + q * PX;
-  const int HW = H * W;
-  typename F::X sx;
-  sx.init(wave, lane, y0 - D, x0 - D, H, W);
-  const rsrc_t rx = plane_rsrc(xs + (size_t)b * C * HW, true, C * HW * 4);
-  auto dma_stage = [&](int st) { sx.load(rx, sm + (st % NS) * XIMG, wave, cbeg + st * CC, cend, HW); };
-  // this wave's DMA instructions per stage (a wave owns the J-th chunk slot of a plane or not)
-  constexpr int J = F::X::J;
-  const bool fullj = wave + (J - 1) * NW < F::X::CHP;
-  const float cf = 1.f / (float)C, fc = (float)C;
-  const bool pow2 = (C & (C - 1)) == 0;
-  float* gxb = gx + (size_t)b * C * HW;
-  const int nst = (cend - cbeg + CC - 1) / CC;
-
-  if (nst > 0) dma_stage(0);
-  if (nst > 1) dma_stage(1);
-  float gv[DYW][2 * D + 1][PX];
-  bwd_load_g<D, PX, SEGX, NW, CC, V, G2, AM>(gv, g + (size_t)b * ep.g_bstride, ep, b, wave, y, xb, H, W);
-  constexpr int GL = DYW * K;
-  static_assert(GL <= bwd_g_loads<D, PX, V, G2, AM, DYW>(), "first wait counts past more loads than bwd_load_g issues");
-  for (int st = 0; st < nst; ++st) {
-    // (a) this wave's share of stage st: younger are the DMAs of stage st + 1
-    // (issued one iteration ago, or in the prologue) and, at st = 0, the g slice
-    const bool next = st + 1 < nst;
-    if (st == 0) {
-      if (next) {
-        if (fullj) dma_wait_le<CC * J + GL>(); else dma_wait_le<CC * (J - 1) + GL>();
-      } else {
-        dma_wait_le<GL>();
-      }
-    } else if (next) {
-      if (fullj) dma_wait_le<CC * J>(); else dma_wait_le<CC * (J - 1)>();
-    } else {
-      dma_wait_all();
-    }
-    flag_publish(LD + wave, st + 1);
-    flags_wait_all<NW>(LD, st + 1);
-    // (b) the FMAs; (c) partials into slot st % 2 once stage st - 2 is combined
-    const float* cur = sm + (st % NS) * XIMG;
-    float* rp = red + (st & 1) * RED1;
-    if (st >= 2) flags_wait_all<NW>(CB, st - 1);
-    bwd_stage<D, PX, SEGX, NW, CC, V, G2>(gv, cur, rp + wave * (CC * TH * TW) + lane * PX, wave, r, q, ep);
-    flag_publish(PD + wave, st + 1);
-    if (st >= 1) {
-      // (e) every wave is done with stage st - 1: combine a third of it, then
-      // refill its x slot with stage st + 2
-      flags_wait_all<NW>(PD, st);
-      bwd_combine<D, PX, SEGX, NW, CC, V>(red + ((st - 1) & 1) * RED1, gxb, threadIdx.x, 64 * NW,
-                                          cbeg + (st - 1) * CC, cend, y0, x0, H, W, cf, fc, pow2);
-      flag_publish(CB + wave, st);
-    }
-    if (st + 2 < nst) dma_stage(st + 2);  // slot (st - 1) % 3: free behind the PD wait above (st >= 1) or unused
-  }
-  if (nst > 0) {
-    flags_wait_all<NW>(PD, nst);
-    bwd_combine<D, PX, SEGX, NW, CC, V>(red + ((nst - 1) & 1) * RED1, gxb, threadIdx.x, 64 * NW,
-                                        cbeg + (nst - 1) * CC, cend, y0, x0, H, W, cf, fc, pow2);
-  }
-}
-
-template <int D, int PX, int SEGX, int NW, int CC, int V, int MODE, bool AM>
-__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(USF_BWD_WAVES_PER_EU))) void corr_bwd_flags_kernel(
-    const float* __restrict__ x1, const float* __restrict__ x2, const float* __restrict__ g, float* __restrict__ gx1,
-    float* __restrict__ gx2, int B, int C, int H, int W, int tiles_x, int cg, BwdEpi ep) {
-  __shared__ __attribute__((aligned(16))) float sm[FlagCfg<D, PX, SEGX, NW, CC, V>::LDSN];
-  {
-    int* fl = reinterpret_cast<int*>(sm + FlagCfg<D, PX, SEGX, NW, CC, V>::LDSN - 16);
-    if (threadIdx.x < 16) fl[threadIdx.x] = 0;
-    __syncthreads();  // the kernel's only workgroup barrier
-  }
-  // work order as corr_bwd_kernel (group fastest, XCD chunks on tile-rich levels)
-  int w = linear_block();
-  if (USF_BWD_CHUNK > 0 && gridDim.x >= 16)
-    w = xcd_chunk(w, gridDim.x * gridDim.y * gridDim.z, USF_BWD_CHUNK);
-  else if (USF_BWD_GROUP_XCD && gridDim.y > 1)
-    w = xcd_chunk(w, gridDim.x * gridDim.y * gridDim.z, gridDim.y);
-  const int group = w % gridDim.y;
-  const int tile = (w / gridDim.y) % gridDim.x;
-  const int b = w / (gridDim.x * gridDim.y);
-  if constexpr (MODE == 1) {
-    corr_bwd_tile_flags<D, PX, SEGX, NW, CC, V, false, AM>(sm, x2, g, gx1, tile, group, b, C, H, W, tiles_x, cg, ep);
-  } else if constexpr (MODE == 2) {
-    corr_bwd_tile_flags<D, PX, SEGX, NW, CC, V, true, AM>(sm, x1, g, gx2, tile, group, b, C, H, W, tiles_x, cg, ep);
-  } else {
-    if (b >= B)
-      corr_bwd_tile_flags<D, PX, SEGX, NW, CC, V, true, AM>(sm, x1, g, gx2, tile, group, b - B, C, H, W, tiles_x,
-                                                            cg, ep);
-    else
-      corr_bwd_tile_flags<D, PX, SEGX, NW, CC, V, false, AM>(sm, x2, g, gx1, tile, group, b, C, H, W, tiles_x, cg,
-                                                             ep);
-  }
-}
-
 // Workgroups a backward launch aims for (both directions together): enough to
 // fill the 256 CUs at 3-4 resident workgroups each, and no more -- every
 // extra channel group re-reads its tile's slice of g (81 planes).
@@ -1607,47 +1445,6 @@ hipError_t launch_bwd_mode(const float* x1, const float* x2, const float* g, flo
   return hipGetLastError();
 }
 
-// the barrier-free backward (corr_bwd_flags_kernel), tile <PX 4, SEGX 8, NW 3>
-template <int D, int CC, int V, int MODE>
-hipError_t launch_bwd_flags_mode(const float* x1, const float* x2, const float* g, float* gx1, float* gx2, int B,
-                                 int C, int H, int W, hipStream_t s, BwdEpi ep) {
-  using F = BwdCfg<D, 4, 8, 3, CC, V>;
-  using FC = FlagCfg<D, 4, 8, 3, CC, V>;
-  constexpr int per_lds = 160 * 1024 / (FC::LDSN * 4);
-  constexpr int PER_CU = per_lds < 3 ? per_lds : 3;
-  const int dirs = MODE == 3 ? 2 : 1;
-  const int tiles_x = (W + F::TW - 1) / F::TW, tiles_y = (H + F::TH - 1) / F::TH;
-  const long units = (long)tiles_x * tiles_y * B * dirs;
-  const long target = (long)kBwdTargetWorkgroups * PER_CU / 3;
-  int groups = (int)((target + units - 1) / units);
-  groups = max(1, min(groups, (C + CC - 1) / CC));
-  const int cg = round_up((C + groups - 1) / groups, CC);
-  dim3 grid(tiles_x * tiles_y, (C + cg - 1) / cg, B * dirs);
-  if (ep.mask)
-    hipLaunchKernelGGL((corr_bwd_flags_kernel<D, 4, 8, 3, CC, V, MODE, true>), grid, dim3(192), 0, s, x1, x2, g, gx1,
-                       gx2, B, C, H, W, tiles_x, cg, ep);
-  else
-    hipLaunchKernelGGL((corr_bwd_flags_kernel<D, 4, 8, 3, CC, V, MODE, false>), grid, dim3(192), 0, s, x1, x2, g,
-                       gx1, gx2, B, C, H, W, tiles_x, cg, ep);
-  return hipGetLastError();
-}
-template <int D, int CC>
-hipError_t launch_bwd_flags(const float* x1, const float* x2, const float* g, float* gx1, float* gx2, int B, int C,
-                            int H, int W, hipStream_t s, BwdEpi ep) {
-  auto by_mode = [&](auto v) {
-    constexpr int V = decltype(v)::value;
-    if (gx1 && gx2) return launch_bwd_flags_mode<D, CC, V, 3>(x1, x2, g, gx1, gx2, B, C, H, W, s, ep);
-    hipError_t e = hipSuccess;
-    if (gx1) e = launch_bwd_flags_mode<D, CC, V, 1>(x1, x2, g, gx1, gx2, B, C, H, W, s, ep);
-    if (e == hipSuccess && gx2) e = launch_bwd_flags_mode<D, CC, V, 2>(x1, x2, g, gx1, gx2, B, C, H, W, s, ep);
-    return e;
-  };
-  if constexpr (Layout<4, 8, D>::X4) {
-    if (W % 4 == 0) return by_mode(std::integral_constant<int, 4>{});
-  }
-  return by_mode(std::integral_constant<int, 1>{});
-}
-
 template <int D, int PX, int SEGX, int NW, int CC, int V, int NB>
 hipError_t launch_bwd_v(const float* x1, const float* x2, const float* g, float* gx1, float* gx2,
                         int B, int C, int H, int W, hipStream_t s, BwdEpi ep) {
@@ -1678,12 +1475,10 @@ hipError_t bwd_candidate_d4(int i, const float* x1, const float* x2, const float
     case 2: return launch_bwd<4, 4, 8, 9, 4>(x1, x2, g, gx1, gx2, B, C, H, W, s, ep);
     case 3: return launch_bwd<4, 4, 8, 9, 8>(x1, x2, g, gx1, gx2, B, C, H, W, s, ep);
     case 4: return launch_bwd<4, 4, 8, 3, 4, 4>(x1, x2, g, gx1, gx2, B, C, H, W, s, ep);
-    case 5: return launch_bwd_flags<4, 2>(x1, x2, g, gx1, gx2, B, C, H, W, s, ep);
-    case 6: return launch_bwd_flags<4, 4>(x1, x2, g, gx1, gx2, B, C, H, W, s, ep);
     default: return hipErrorInvalidValue;
   }
 }
-constexpr int kBwdCandidates = 7;
+constexpr int kBwdCandidates = 5;
 
 // Small grids take the 4-image ring: at most this many (tile, direction, sample)
 // units. There every workgroup's channel loop is short (2-6 stages), and with
@@ -1707,7 +1502,6 @@ hipError_t bwd_dispatch(const float* x1, const float* x2, const float* g, float*
   using T = BwdCfg<D, 4, 8, 3, 4, 1>;  // the default tile (32 x 8)
   const long units = (long)((W + T::TW - 1) / T::TW) * ((H + T::TH - 1) / T::TH) * B * ((gx1 && gx2) ? 2 : 1);
   if (units <= USF_BWD_RING_UNITS) return launch_bwd<D, 4, 8, 3, 4, 4>(x1, x2, g, gx1, gx2, B, C, H, W, s, ep);
-  if (USF_BWD_FLAGS) return launch_bwd_flags<D, 2>(x1, x2, g, gx1, gx2, B, C, H, W, s, ep);
   return launch_bwd<D>(x1, x2, g, gx1, gx2, B, C, H, W, s, ep);
 }
 
