@@ -1383,7 +1383,9 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(USF_BWD
     // In the linear order the groups of a tile are consecutive blocks, i.e. on
     // different XCDs, so every group misses its own L2 (PMC traffic 2.7x of
     // algorithmic at L2). One XCD chunk per tile's groups.
-    w = xcd_chunk(w, gridDim.x * gridDim.y * gridDim.z, gridDim.y);
+    // (USF_BWD_GROUP_XCD=2: all tiles and groups of a (sample, direction) on one
+    // XCD, so neighbouring tiles' shared x halo rows hit one L2 as well)
+    w = xcd_chunk(w, gridDim.x * gridDim.y * gridDim.z, USF_BWD_GROUP_XCD == 2 ? gridDim.x * gridDim.y : gridDim.y);
   }
   int group, tile, b;
   if (dirfast) {

@@ -275,30 +275,13 @@ __device__ __forceinline__ TapB make_tap_b(float u, float v, int x, int y, int H
 // workgroup (USF_PHOTO_PAIRS=2) both stream the same strip rows (the two
 // directions, or two neighbouring strips), so they take the same number of
 // steps and barriers.
-// USF_PHOTO_FLAGS = 1: no workgroup barrier per step. The pair hands rows over
-// through two step counters in LDS (the producer's rows written, the
-// consumer's steps done); each wave waits only when it would overtake the
-// other, so the producer runs up to kRing - 3 steps ahead instead of in
-// lockstep. The ring then holds 6 rows.
-#ifndef USF_PHOTO_FLAGS
-#define USF_PHOTO_FLAGS 0
-#endif
-constexpr int kRing = USF_PHOTO_FLAGS ? 6 : 4;
-// ring slot of strip row j (a power-of-two ring masks, the six-row ring divides)
-__device__ __forceinline__ int ring_slot(int j) { return (kRing & (kRing - 1)) == 0 ? j & (kRing - 1) : j % kRing; }
-// step-counter handshake (USF_PHOTO_FLAGS) on an LDS word. Only LDS data is
-// handed over, so the publishing wave waits for its own LDS writes
-// (lgkmcnt), not for its global basis stores as a release fence would; the
-// reader's data loads are issued after its poll returned (control dependence,
-// and the asm keeps the compiler from hoisting them).
-__device__ __forceinline__ void flag_set(int* f, int v) {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __hip_atomic_store(f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ __forceinline__ void flag_wait_ge(int* f, int v) {
-  while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < v) __builtin_amdgcn_s_sleep(1);
-  asm volatile("" ::: "memory");
-}
+constexpr int kRing = 4;
+// (Round 5 built the pair without a workgroup barrier per step: two step
+// counters in LDS and a six-row ring, so the producer could run three rows
+// ahead. Full resolution with the gradient basis: 55.6-56.0 vs 55.4-56.3 us,
+// smaller scales 0.3-0.6 us slower; forward only 35.3 vs 37.7 us.
+// profiles/ab_r05/photo_flags.json; not kept: the step is not set by the
+// barrier handshake.)
 // producer/consumer pairs per workgroup. One: each pair's barrier waits for its
 // own two waves only. Two pairs per 256-thread workgroup (round 3) kept both
 // pairs in step; one pair measured 0.3-1.3 us faster at every loss scale
@@ -320,7 +303,6 @@ struct PairCommon {
   bool col_in, lane_own, wcol;
   float* xy;  // this pair's LDS ring: [kRing][C][2][64] (x, y planes)
   float* pd;  // [kRing][C][2][64] (dix kx, diy ky planes)
-  int* fl;    // USF_PHOTO_FLAGS: [0] producer rows written, [1] consumer steps done
   __device__ __forceinline__ void st(float v, int off, int soff) {
     __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(int, v), rbas, off, soff, 0);
   }
@@ -423,10 +405,7 @@ struct Producer : PairCommon<BORDER, GRAD, C> {
       }
       msum += mo;
     }
-    const int slot = ring_slot(i);
-    // the slot held row i - kRing, which the consumer reads at its steps
-    // i - kRing (new row) and i - kRing + 2 (basis row)
-    if (USF_PHOTO_FLAGS) flag_wait_ge(this->fl + 1, i - kRing + 3);
+    const int slot = i & (kRing - 1);
 #pragma unroll
     for (int c = 0; c < C; ++c) {
       this->xy[this->ring(slot, c, 0)] = x[c];
@@ -441,10 +420,7 @@ struct Producer : PairCommon<BORDER, GRAD, C> {
       this->st(ax * kx, o, 0);
       this->st(ay * ky, o, 4 * this->HW);
     }
-    if (USF_PHOTO_FLAGS)
-      flag_set(this->fl, i + 1);  // row i is in the ring (LDS writes of one wave land in order)
-    else
-      __syncthreads();
+    __syncthreads();
   }
 };
 
@@ -460,8 +436,7 @@ struct Consumer : PairCommon<BORDER, GRAD, C> {
   __device__ __forceinline__ void step(int j) {
     constexpr int S0 = PH, S1 = (PH + 2) % 3, S2 = (PH + 1) % 3;
     const int r = this->y0 - 2 + j;
-    const int slot = ring_slot(j), slot2 = ring_slot(j - 2 + kRing);
-    if (USF_PHOTO_FLAGS) flag_wait_ge(this->fl, j + 1);  // the producer's row j
+    const int slot = j & (kRing - 1), slot2 = (j - 2) & (kRing - 1);
     float x[C], y[C];
 #pragma unroll
     for (int c = 0; c < C; ++c) {
@@ -519,10 +494,7 @@ struct Consumer : PairCommon<BORDER, GRAD, C> {
       this->st(bx, o, 8 * this->HW);
       this->st(by, o, 12 * this->HW);
     }
-    if (USF_PHOTO_FLAGS)
-      flag_set(this->fl + 1, j + 1);  // rows j and j - 2 read (their values are in registers)
-    else
-      __syncthreads();
+    __syncthreads();
   }
 };
 
@@ -535,7 +507,6 @@ __device__ __forceinline__ float wave_sum(float v) {
 template <bool BORDER, bool GRAD, int C>
 __global__ __launch_bounds__(128 * kPairs) __attribute__((amdgpu_waves_per_eu(USF_PHOTO_EU))) void photo_pc_kernel(StripArgs a, float* __restrict__ partials) {
   __shared__ float lds[kPairs][2][kRing * C * 2 * 64];  // [pair][x,y | gradient state]
-  __shared__ int flags[kPairs][2];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int pair = wave >> 1;
@@ -552,11 +523,6 @@ __global__ __launch_bounds__(128 * kPairs) __attribute__((amdgpu_waves_per_eu(US
   const int y0 = (int)((long long)sy * H / a.nsy);
   const int rown = (int)((long long)(sy + 1) * H / a.nsy) - y0;
   const int nsteps = rown + 4;  // the same for both pairs (same strip row)
-  if (USF_PHOTO_FLAGS) {
-    static_assert(!USF_PHOTO_FLAGS || kPairs == 1, "the step-counter handshake is per pair");
-    if (threadIdx.x < 2) flags[0][threadIdx.x] = 0;
-    __syncthreads();  // the only barrier of the flag form
-  }
   if (!valid) {  // keep the barrier count of the other pair
     for (int i = 0; i <= nsteps; ++i) __syncthreads();
     return;
@@ -579,7 +545,6 @@ __global__ __launch_bounds__(128 * kPairs) __attribute__((amdgpu_waves_per_eu(US
     p.wcol = p.col >= 0 && p.col <= W - 3;
     p.xy = lds[pair][0];
     p.pd = lds[pair][1];
-    p.fl = flags[pair];
     if constexpr (GRAD) p.rbas = __builtin_amdgcn_make_buffer_rsrc(dr.basis + b * a.bbs, 0, 16 * HW, kRsrcWord3);
   };
   float* po = partials + 3 * (((size_t)dirn * a.B + b) * a.nsy * a.nsx + (size_t)sy * a.nsx + sx);
@@ -612,7 +577,7 @@ __global__ __launch_bounds__(128 * kPairs) __attribute__((amdgpu_waves_per_eu(US
     if (i + 1 < nsteps) P.template step<0, 2>(i + 1, nsteps);
     if (i + 2 < nsteps) P.template step<1, 2>(i + 2, nsteps);
     if (i + 3 < nsteps) P.template step<2, 2>(i + 3, nsteps);
-    if (!USF_PHOTO_FLAGS) __syncthreads();  // the consumer's last step
+    __syncthreads();  // the consumer's last step
     const float l1 = wave_sum(P.l1), ms = wave_sum(P.msum);
     if (lane == 0) {
       po[0] = l1;
@@ -629,7 +594,7 @@ __global__ __launch_bounds__(128 * kPairs) __attribute__((amdgpu_waves_per_eu(US
         Q.ca[k][c] = Q.cb[k][c] = Q.cg[k][c] = 0.f;
       }
     Q.ssum = 0.f;
-    if (!USF_PHOTO_FLAGS) __syncthreads();  // the producer's first row
+    __syncthreads();  // the producer's first row
     Q.template step<0, 0, 0>(0);
     Q.template step<1, 0, 0>(1);
     Q.template step<2, 2, 0>(2);

@@ -329,7 +329,20 @@ __device__ __forceinline__ bool gather_inlier(float u, float v) {
 // cell: strongly compressive flow, or border clamping) are listed and added
 // afterwards with float atomics.
 constexpr int kBinSlots = 4;
-constexpr int kBinTW = 32, kBinTH = 8;  // target tile of the gather pass (warp_gx_bins_kernel)
+constexpr int kBinTW = 32, kBinTH = 8;
+// A parity word of the persistent workspace, read with a VECTOR buffer load:
+// it then waits in vmcnt beside the kernel's first data loads instead of a
+// scalar load that the kernel-argument wait serialises in front of them.
+__device__ __forceinline__ int hdr_word(const int* hdr, int i) {
+  const auto r = __builtin_amdgcn_make_buffer_rsrc(const_cast<int*>(hdr), 0, 8, 0x00020000);
+  return __builtin_amdgcn_raw_buffer_load_b32(r, 4 * i, 0, 0);
+}
+// the parity at its use: kept in a VGPR (the asm hides its uniformity, so no
+// v_readfirstlane is hoisted to the load), the wait sits here
+__device__ __forceinline__ int at_use(int v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}  // target tile of the gather pass (warp_gx_bins_kernel)
 struct BinArgs {
   int* cnt = nullptr;      // [B][(H+1)(W+1)] pixels filed per cell
   int* bins = nullptr;     // [B][(H+1)(W+1)][kBinSlots] source pixel (py << 16 | px)
@@ -360,6 +373,9 @@ __global__ __launch_bounds__(256) void warp_bwd_kernel(const float* __restrict__
                                                        int H, int W, BinArgs ba = {}) {
   constexpr int PXB = 256 / CS;
   __shared__ float red[2][256];
+  // BIN == 2: this call's count-buffer parity, loaded first so its latency
+  // overlaps the flow loads (the filing atomics need both)
+  const int par = BIN == 2 ? hdr_word(ba.hdr, 0) : 0;
   const int HW = H * W;
   const int t = threadIdx.x;
   const int slice = t / PXB;
@@ -380,17 +396,13 @@ __global__ __launch_bounds__(256) void warp_bwd_kernel(const float* __restrict__
   if (!valid) tp.m_nw = tp.m_ne = tp.m_sw = tp.m_se = false;
   if (OUTL && !__syncthreads_or(valid)) return;  // no outlier in this workgroup (uniform)
   bool ovf = false;  // BIN == 2: p did not get a slot; its contributions go to ba.ovfgx
-  if (BIN == 2) {
-    // parity of this call's count buffer; handed to the gather (which flips it for the next call)
-    const int par = __builtin_amdgcn_readfirstlane(*(volatile const int*)ba.hdr);
-    ba.cnt = ba.cnt2 + (size_t)par * ba.ncell;
-    if (t == 0) ba.hdr[1] = par;
-  }
   if (BIN && slice == 0 && valid) {
     // file p under its north-west corner cell (see BinArgs); weights as the scatter forms them
     if (tp.m_nw || tp.m_ne || tp.m_sw || tp.m_se) {  // then xw in [-1, W), yn in [-1, H)
       const size_t cell = (size_t)b * (H + 1) * (W + 1) + (size_t)(tp.yn + 1) * (W + 1) + (tp.xw + 1);
-      const int slot = atomicAdd(ba.cnt + cell, 1);
+      // BIN == 2: this call's count buffer, the one the parity selects
+      int* cnt = BIN == 2 ? ba.cnt2 + (size_t)at_use(par) * ba.ncell : ba.cnt;
+      const int slot = atomicAdd(cnt + cell, 1);
       if (slot < kBinSlots) {
         ba.bins[cell * kBinSlots + slot] = (p / W) << 16 | (p % W);  // (py, px): sorts as p
         float* wb = ba.wbin + cell * kBinSlots + slot;
@@ -417,23 +429,27 @@ __global__ __launch_bounds__(256) void warp_bwd_kernel(const float* __restrict__
       }
     }
   }
-  RowRuns ron{}, ros{};  // BIN == 2: reduce-by-key runs of the overflow pixels' corner rows
-  bool wave_ovf = false;
-  if (BIN == 2) {
-    __shared__ unsigned char ovf_s[PXB];
-    if (slice == 0) ovf_s[pl] = ovf;
-    __syncthreads();
-    ovf = ovf_s[pl] != 0;
-    wave_ovf = __any(ovf);
-    if (wave_ovf) {  // wave-uniform: every lane takes part in the shuffles
-      const int lane = t & 63;
-      const bool has_left = pl > 0 && lane != 0, has_right = pl + 1 < PXB && lane != 63;
-      const bool vx = ovf && tp.xw >= -1 && tp.xw < W;
-      const bool vyn = vx && (unsigned)tp.yn < (unsigned)H, vys = vx && (unsigned)(tp.yn + 1) < (unsigned)H;
-      ron = row_runs(vyn ? tp.yn * (W + 1) + tp.xw + 1 : -(lane + 2), ovf && tp.m_nw, ovf && tp.m_ne, has_left,
-                     has_right);
-      ros = row_runs(vys ? (tp.yn + 1) * (W + 1) + tp.xw + 1 : -(lane + 2), ovf && tp.m_sw, ovf && tp.m_se,
-                     has_left, has_right);
+  if (BIN == 2 && t == 0) ba.hdr[1] = at_use(par);  // handed to the gather, which flips hdr[0] for the next call
+  if (BIN == 2 && __any(ovf)) {
+    // Overflow pixels (rare: strongly compressive flow, border piles) are
+    // scattered by their filing lane itself, all channels, into ba.ovfgx with the
+    // reduce-by-key atomics (wave-uniform branch: every lane takes part in the
+    // shuffles); the other slices never wait for the filing atomics.
+    const int lane = t & 63;
+    const bool has_left = pl > 0 && lane != 0, has_right = pl + 1 < PXB && lane != 63;
+    const bool vx = ovf && tp.xw >= -1 && tp.xw < W;
+    const bool vyn = vx && (unsigned)tp.yn < (unsigned)H, vys = vx && (unsigned)(tp.yn + 1) < (unsigned)H;
+    const RowRuns ron = row_runs(vyn ? tp.yn * (W + 1) + tp.xw + 1 : -(lane + 2), ovf && tp.m_nw, ovf && tp.m_ne,
+                                 has_left, has_right);
+    const RowRuns ros = row_runs(vys ? (tp.yn + 1) * (W + 1) + tp.xw + 1 : -(lane + 2), ovf && tp.m_sw,
+                                 ovf && tp.m_se, has_left, has_right);
+    const float wnw = tp.s * tp.e, wne = tp.s * tp.w, wsw = tp.n * tp.e, wse = tp.n * tp.w;
+    const float* gp = gout + (size_t)b * C * HW + (ovf ? p : 0);
+    for (int c = 0; c < C; ++c) {
+      const float go = ovf ? gp[(size_t)c * HW] : 0.f;
+      float* oc = ba.ovfgx + ((size_t)b * C + c) * HW;
+      scatter_row(oc, tp.o_nw, tp.o_ne, ovf && tp.m_nw, ovf && tp.m_ne, go * wnw, go * wne, ron);
+      scatter_row(oc, tp.o_sw, tp.o_se, ovf && tp.m_sw, ovf && tp.m_se, go * wsw, go * wse, ros);
     }
   }
   // grad_x: reduce-by-key over the wave per corner row (see scatter_row)
@@ -467,11 +483,6 @@ __global__ __launch_bounds__(256) void warp_bwd_kernel(const float* __restrict__
         float* gc = gxb + (size_t)c * HW;
         scatter_row(gc, tp.o_nw, tp.o_ne, tp.m_nw, tp.m_ne, go * wnw, go * wne, rn);
         scatter_row(gc, tp.o_sw, tp.o_se, tp.m_sw, tp.m_se, go * wsw, go * wse, rs);
-      }
-      if (BIN == 2 && wave_ovf) {
-        float* oc = ba.ovfgx + ((size_t)b * C + c) * HW;
-        scatter_row(oc, tp.o_nw, tp.o_ne, ovf && tp.m_nw, ovf && tp.m_ne, go * wnw, go * wne, ron);
-        scatter_row(oc, tp.o_sw, tp.o_se, ovf && tp.m_sw, ovf && tp.m_se, go * wsw, go * wse, ros);
       }
       if (WANT_GF && valid) {
         const float* xc = xb + (size_t)c * HW;
@@ -539,18 +550,12 @@ __global__ __launch_bounds__(256) void warp_gx_bins_kernel(const float* __restri
   const int c0 = blockIdx.z * cper, c1 = min(C, c0 + cper);
   const bool valid = qy < H && qx < W;
   const int qq = valid ? qy * W + qx : 0;
-  bool dirty = false;  // PERSIST: this (tile, channel group) has overflow contributions to add
-  if (PERSIST) {
-    // this call's counts (the parity the filing pass handed over); the other
-    // buffer is zeroed here for the next call, which reads the flipped parity
-    const int par = __builtin_amdgcn_readfirstlane(*(volatile const int*)(ba.hdr + 1));
-    ba.cnt = ba.cnt2 + (size_t)par * ba.ncell;
-    int* other = ba.cnt2 + (size_t)(1 - par) * ba.ncell;
-    const long long nth = (long long)gridDim.x * gridDim.y * gridDim.z * 256;
-    for (long long i = (long long)linear_block() * 256 + t; i < ba.ncell; i += nth) other[i] = 0;
-    if (t == 0) ba.hdr[0] = 1 - par;
-    dirty = (ba.dirty[(size_t)b * ba.ntiles + blockIdx.x] >> blockIdx.z) & 1u;
-  }
+  // PERSIST: this call's count buffer is the one the filing pass's parity
+  // selects; both buffers' counts are loaded beside the parity (no dependent
+  // load before the gather's own), and the other buffer is zeroed at the end
+  // for the next call, which reads the flipped parity
+  const int par = PERSIST ? hdr_word(ba.hdr, 1) : 0;
+  const unsigned dword = PERSIST ? ba.dirty[(size_t)b * ba.ntiles + blockIdx.x] : 0u;
   if (t == 0) {
     bb[0] = INT_MAX; bb[1] = INT_MIN; bb[2] = INT_MAX; bb[3] = INT_MIN;
   }
@@ -565,7 +570,15 @@ __global__ __launch_bounds__(256) void warp_gx_bins_kernel(const float* __restri
     // count, slots and the slots' weights load together (slots 0 and 1
     // unconditionally: most cells hold at most two pixels)
     const size_t ce = valid ? cell : 0;
-    const int n = valid ? min(ba.cnt[ce], kBinSlots) : 0;
+    int cn;
+    if (PERSIST) {
+      int ca = ba.cnt2[ce], cb = ba.cnt2[ba.ncell + ce];
+      asm volatile("" : "+v"(ca), "+v"(cb));  // both loads issue: no select-then-load behind the parity
+      cn = at_use(par) ? cb : ca;
+    } else {
+      cn = ba.cnt[ce];
+    }
+    const int n = valid ? min(cn, kBinSlots) : 0;
     const int4 e4 = *reinterpret_cast<const int4*>(ba.bins + ce * kBinSlots);
     // the 4 slots' weights for this corner: one 16-byte load (corner-major layout)
     const float4 w4 = *reinterpret_cast<const float4*>(ba.wbin + ((size_t)k * ba.ncell + ce) * kBinSlots);
@@ -683,7 +696,8 @@ __global__ __launch_bounds__(256) void warp_gx_bins_kernel(const float* __restri
             for (int u = 0; u < kGatherCH; ++u) acc[u] = fmaf(wk[k][j], src[co[u]], acc[u]);
           }
     }
-    if (PERSIST && dirty && valid) {
+    const bool dirty = PERSIST && ((dword >> blockIdx.z) & 1u);  // overflow to add for this channel group
+    if (dirty && valid) {
       // the overflow pixels' contributions (scattered by the filing pass), then
       // re-zeroed: this workgroup is their only reader
       float* oq = ba.ovfgx + (size_t)b * C * HW + qq;
@@ -700,7 +714,15 @@ __global__ __launch_bounds__(256) void warp_gx_bins_kernel(const float* __restri
         if (c + u < c1) gq[(size_t)(c + u) * HW] = acc[u];
     }
   }
-  if (PERSIST && dirty && t == 0) atomicAnd(ba.dirty + (size_t)b * ba.ntiles + blockIdx.x, ~(1u << blockIdx.z));
+  if (PERSIST) {
+    if (((dword >> blockIdx.z) & 1u) && t == 0)
+      atomicAnd(ba.dirty + (size_t)b * ba.ntiles + blockIdx.x, ~(1u << blockIdx.z));
+    const int pv = at_use(par);  // (a VGPR: no scalar copy of the parity is hoisted to its load)
+    int* other = ba.cnt2 + (size_t)(1 - pv) * ba.ncell;
+    const long long nth = (long long)gridDim.x * gridDim.y * gridDim.z * 256;
+    for (long long i = (long long)linear_block() * 256 + t; i < ba.ncell; i += nth) other[i] = 0;
+    if (linear_block() == 0 && t == 0) ba.hdr[0] = 1 - pv;
+  }
 }
 
 // Overflow pixels of the binned grad_x add their four corner contributions
