@@ -996,6 +996,11 @@ struct BwdCfg {
 #ifndef USF_BWD_EARLY
 #define USF_BWD_EARLY 1
 #endif
+// Wave issue priority in the stage loop (A/B knob): 1 = raised during the FMAs,
+// 2 = raised while issuing the next stage's DMA; 0 = never.
+#ifndef USF_BWD_PRIO
+#define USF_BWD_PRIO 0
+#endif
 // Occupancy target of the backward kernels (see corr_bwd_kernel).
 #ifndef USF_BWD_WAVES_PER_EU
 #define USF_BWD_WAVES_PER_EU 3
@@ -1312,10 +1317,14 @@ __device__ __forceinline__ void corr_bwd_tile(float* sm, const float* __restrict
       __syncthreads();  // stage st landed; partial slices free
     }
     USF_TRACE_AT(3 + 5 * st);
+    if (USF_BWD_PRIO == 2) __builtin_amdgcn_s_setprio(2);
     if (st + NB - 1 < nst) dma_stage(cbeg + (st + NB - 1) * CC, sm + wr * XIMG);
+    if (USF_BWD_PRIO == 2) __builtin_amdgcn_s_setprio(0);
     const float* cur = sm + rd * XIMG;
     USF_TRACE_AT(4 + 5 * st);
+    if (USF_BWD_PRIO == 1) __builtin_amdgcn_s_setprio(2);
     bwd_stage<D, PX, SEGX, NW, CC, V, G2>(gv, cur, red + wave * (CC * TH * TW) + lane * PX, wave, r, q, ep);
+    if (USF_BWD_PRIO == 1) __builtin_amdgcn_s_setprio(0);
     USF_TRACE_AT(5 + 5 * st);
     if (!TOPWAIT) dma_wait_all();  // stage st + 1 (NB == 2: nothing else in flight)
     USF_TRACE_AT(6 + 5 * st);
@@ -1359,6 +1368,9 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(USF_BWD
 #ifndef USF_BWD_GROUP_XCD
 #define USF_BWD_GROUP_XCD 1
 #endif
+#ifndef USF_BWD_SAMPLE_RING
+#define USF_BWD_SAMPLE_RING 1
+#endif
 #ifndef USF_BWD_DIRFAST_CHUNK
 #define USF_BWD_DIRFAST_CHUNK 28
 #endif
@@ -1369,7 +1381,15 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(USF_BWD
   // at the same replayed time (69.9 vs 67.8 us), but 6 us slower inside the
   // training step (rocprof: 75.7 vs 69.6 us, profiles/r02_v3_*): off by default.
   const bool dirfast = MODE == 3 && USF_BWD_DIRFAST && USF_BWD_CHUNK > 0 && gridDim.x >= 16;
-  if (USF_BWD_CHUNK > 0 && gridDim.x >= 16) {
+  const int nitems = gridDim.x * gridDim.y * gridDim.z;
+  const int per_sample = gridDim.x * gridDim.y;  // work items of one (sample, direction)
+  if (NB > 2 && USF_BWD_SAMPLE_RING && nitems >= 8 * per_sample) {
+    // small (four-image ring) grids: every item of a (sample, direction) -- its
+    // tiles, whose x halo rows overlap, and their channel groups, which all
+    // load the tile's g slice -- on one XCD (USF_BWD_SAMPLE_RING; KITTI L2 PMC
+    // traffic 2.13x -> 1.02x, 25.5 -> 23.7 us, profiles/ab_r05/corr_bwd_sample_xcd.json)
+    w = xcd_chunk(w, nitems, per_sample);
+  } else if (USF_BWD_CHUNK > 0 && gridDim.x >= 16) {
     // Q consecutive work items per XCD, chunks dealt round-robin over the 8
     // XCDs (block lin runs on XCD lin % 8; it gets item Q (8 m + x) + j): a few
     // neighbouring tiles share their halo lines in one L2 while every XCD still
@@ -1378,14 +1398,12 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(USF_BWD
     // slower (84 us) and so are levels with < 16 tiles (L1 11.6 -> 13.5 us).
     w = xcd_chunk(w, gridDim.x * gridDim.y * gridDim.z, dirfast ? USF_BWD_DIRFAST_CHUNK : USF_BWD_CHUNK);
   } else if (USF_BWD_GROUP_XCD && gridDim.y > 1) {
-    // Small grids (KITTI L0-L2, the four-image ring) split a tile's channels over
-    // gridDim.y groups, each of which loads the tile's whole g slice (81 planes).
-    // In the linear order the groups of a tile are consecutive blocks, i.e. on
-    // different XCDs, so every group misses its own L2 (PMC traffic 2.7x of
-    // algorithmic at L2). One XCD chunk per tile's groups.
-    // (USF_BWD_GROUP_XCD=2: all tiles and groups of a (sample, direction) on one
-    // XCD, so neighbouring tiles' shared x halo rows hit one L2 as well)
-    w = xcd_chunk(w, gridDim.x * gridDim.y * gridDim.z, USF_BWD_GROUP_XCD == 2 ? gridDim.x * gridDim.y : gridDim.y);
+    // Otherwise small grids that split a tile's channels over gridDim.y groups
+    // (each loads the tile's whole g slice): one XCD chunk per tile's groups. In
+    // the linear order they were consecutive blocks on different XCDs, every
+    // group missing its own L2 (L0 1.89x -> 1.17x, L1 2.06x -> 1.06x,
+    // profiles/ab_r05/corr_bwd_group_xcd.json).
+    w = xcd_chunk(w, nitems, gridDim.y);
   }
   int group, tile, b;
   if (dirfast) {

@@ -430,28 +430,6 @@ __global__ __launch_bounds__(256) void warp_bwd_kernel(const float* __restrict__
     }
   }
   if (BIN == 2 && t == 0) ba.hdr[1] = at_use(par);  // handed to the gather, which flips hdr[0] for the next call
-  if (BIN == 2 && __any(ovf)) {
-    // Overflow pixels (rare: strongly compressive flow, border piles) are
-    // scattered by their filing lane itself, all channels, into ba.ovfgx with the
-    // reduce-by-key atomics (wave-uniform branch: every lane takes part in the
-    // shuffles); the other slices never wait for the filing atomics.
-    const int lane = t & 63;
-    const bool has_left = pl > 0 && lane != 0, has_right = pl + 1 < PXB && lane != 63;
-    const bool vx = ovf && tp.xw >= -1 && tp.xw < W;
-    const bool vyn = vx && (unsigned)tp.yn < (unsigned)H, vys = vx && (unsigned)(tp.yn + 1) < (unsigned)H;
-    const RowRuns ron = row_runs(vyn ? tp.yn * (W + 1) + tp.xw + 1 : -(lane + 2), ovf && tp.m_nw, ovf && tp.m_ne,
-                                 has_left, has_right);
-    const RowRuns ros = row_runs(vys ? (tp.yn + 1) * (W + 1) + tp.xw + 1 : -(lane + 2), ovf && tp.m_sw,
-                                 ovf && tp.m_se, has_left, has_right);
-    const float wnw = tp.s * tp.e, wne = tp.s * tp.w, wsw = tp.n * tp.e, wse = tp.n * tp.w;
-    const float* gp = gout + (size_t)b * C * HW + (ovf ? p : 0);
-    for (int c = 0; c < C; ++c) {
-      const float go = ovf ? gp[(size_t)c * HW] : 0.f;
-      float* oc = ba.ovfgx + ((size_t)b * C + c) * HW;
-      scatter_row(oc, tp.o_nw, tp.o_ne, ovf && tp.m_nw, ovf && tp.m_ne, go * wnw, go * wne, ron);
-      scatter_row(oc, tp.o_sw, tp.o_se, ovf && tp.m_sw, ovf && tp.m_se, go * wsw, go * wse, ros);
-    }
-  }
   // grad_x: reduce-by-key over the wave per corner row (see scatter_row)
   RowRuns rn{}, rs{};
   if (WANT_GX) {
@@ -492,6 +470,48 @@ __global__ __launch_bounds__(256) void warp_bwd_kernel(const float* __restrict__
         const float vse = tp.m_se ? xc[tp.o_se] : 0.f;
         dix += ((vne - vnw) * tp.s + (vse - vsw) * tp.n) * go;
         diy += ((vsw - vnw) * tp.e + (vse - vne) * tp.w) * go;
+      }
+    }
+  }
+  if (BIN == 2) {
+    // Overflow pixels (rare: strongly compressive flow, border piles) go to
+    // ba.ovfgx with the reduce-by-key atomics. Only the filing lane knows its
+    // pixel overflowed; the barrier sits after the channel loop, so no slice
+    // ever waits for the filing atomics, and each slice then scatters its own
+    // channels with its loads batched (no load round trip per channel).
+    __shared__ unsigned char ovf_s[PXB];
+    if (slice == 0) ovf_s[pl] = ovf;
+    __syncthreads();
+    const bool po = ovf_s[pl] != 0;
+    if (__any(po)) {  // wave-uniform: every lane takes part in the shuffles
+      const int lane = t & 63;
+      const bool has_left = pl > 0 && lane != 0, has_right = pl + 1 < PXB && lane != 63;
+      const bool vx = po && tp.xw >= -1 && tp.xw < W;
+      const bool vyn = vx && (unsigned)tp.yn < (unsigned)H, vys = vx && (unsigned)(tp.yn + 1) < (unsigned)H;
+      const RowRuns ron = row_runs(vyn ? tp.yn * (W + 1) + tp.xw + 1 : -(lane + 2), po && tp.m_nw, po && tp.m_ne,
+                                   has_left, has_right);
+      const RowRuns ros = row_runs(vys ? (tp.yn + 1) * (W + 1) + tp.xw + 1 : -(lane + 2), po && tp.m_sw,
+                                   po && tp.m_se, has_left, has_right);
+      const float wnw = tp.s * tp.e, wne = tp.s * tp.w, wsw = tp.n * tp.e, wse = tp.n * tp.w;
+      const float* gp = gout + (size_t)b * C * HW + (po ? p : 0);
+      // a wave-uniform loop (a wave may hold several slices): lane channel
+      // c = base + slice + j * CS, masked past C, so every lane runs every shuffle
+      constexpr int NB8 = 8;
+      for (int base = 0; base < C; base += NB8 * CS) {
+        float go[NB8];
+#pragma unroll
+        for (int j = 0; j < NB8; ++j) {
+          const int c = base + slice + j * CS;
+          go[j] = po && c < C ? gp[(size_t)c * HW] : 0.f;
+        }
+#pragma unroll
+        for (int j = 0; j < NB8; ++j) {
+          const int c = base + slice + j * CS;
+          const bool cv = po && c < C;
+          float* oc = ba.ovfgx + ((size_t)b * C + min(c, C - 1)) * HW;
+          scatter_row(oc, tp.o_nw, tp.o_ne, cv && tp.m_nw, cv && tp.m_ne, go[j] * wnw, go[j] * wne, ron);
+          scatter_row(oc, tp.o_sw, tp.o_se, cv && tp.m_sw, cv && tp.m_se, go[j] * wsw, go[j] * wse, ros);
+        }
       }
     }
   }
@@ -555,6 +575,9 @@ __global__ __launch_bounds__(256) void warp_gx_bins_kernel(const float* __restri
   // load before the gather's own), and the other buffer is zeroed at the end
   // for the next call, which reads the flipped parity
   const int par = PERSIST ? hdr_word(ba.hdr, 1) : 0;
+  // both count buffers (2 x ncell ints < 2 GiB: capi.cpp bounds the shapes)
+  const auto crs = __builtin_amdgcn_make_buffer_rsrc(PERSIST ? ba.cnt2 : ba.cnt, 0,
+                                                     (int)(PERSIST ? 8 * ba.ncell : 4), 0x00020000);
   const unsigned dword = PERSIST ? ba.dirty[(size_t)b * ba.ntiles + blockIdx.x] : 0u;
   if (t == 0) {
     bb[0] = INT_MAX; bb[1] = INT_MIN; bb[2] = INT_MAX; bb[3] = INT_MIN;
@@ -572,8 +595,10 @@ __global__ __launch_bounds__(256) void warp_gx_bins_kernel(const float* __restri
     const size_t ce = valid ? cell : 0;
     int cn;
     if (PERSIST) {
-      int ca = ba.cnt2[ce], cb = ba.cnt2[ba.ncell + ce];
-      asm volatile("" : "+v"(ca), "+v"(cb));  // both loads issue: no select-then-load behind the parity
+      // both buffers' counts by buffer-load intrinsics: the compiler cannot fold
+      // the parity select into one load's address (a load behind the parity load)
+      const int ca = __builtin_amdgcn_raw_buffer_load_b32(crs, (int)(4 * ce), 0, 0);
+      const int cb = __builtin_amdgcn_raw_buffer_load_b32(crs, (int)(4 * (ba.ncell + ce)), 0, 0);
       cn = at_use(par) ? cb : ca;
     } else {
       cn = ba.cnt[ce];
