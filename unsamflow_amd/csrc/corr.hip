@@ -951,8 +951,11 @@ hipError_t fwd_dispatch(const float* x1, const float* x2, float* out, int B, int
   }
   // unsplit mid-size grids: two channel slices per workgroup on shared stages
   // (profiles/ab_r02/fwd_slices.json: KITTI L2 18.3 -> 14.6 us, SURVEY config 1
-  // 9.3 -> 8.2 us with CC = 8; config 2 (C = 128) 25.7 -> 24.4 us with CC = 4)
-  if (C >= 128) return launch_fwd<D, 4, 8, 3, 4, 2>(x1, x2, out, B, C, H, W, s, ep);
+  // 9.3 -> 8.2 us with CC = 8). At C >= 128 (only SURVEY config 2 reaches this
+  // path) one slice with CC = 8: from cold caches 28.0 vs 33.1 us (two slices
+  // of CC = 4), warm 25.4 vs 23.9 us (profiles/ab_r05/corr_fwd_variants.json);
+  // the cold figure is the HBM-honest one.
+  if (C >= 128) return launch_fwd<D, 4, 8, 3, 8>(x1, x2, out, B, C, H, W, s, ep);
   return launch_fwd<D, 4, 8, 3, 8, 2>(x1, x2, out, B, C, H, W, s, ep);
 }
 
@@ -995,11 +998,6 @@ struct BwdCfg {
 // barrier waits only for it (corr_bwd_tile); 0: both waited for (vmcnt(0)).
 #ifndef USF_BWD_EARLY
 #define USF_BWD_EARLY 1
-#endif
-// Wave issue priority in the stage loop (A/B knob): 1 = raised during the FMAs,
-// 2 = raised while issuing the next stage's DMA; 0 = never.
-#ifndef USF_BWD_PRIO
-#define USF_BWD_PRIO 0
 #endif
 // Occupancy target of the backward kernels (see corr_bwd_kernel).
 #ifndef USF_BWD_WAVES_PER_EU
@@ -1317,14 +1315,10 @@ __device__ __forceinline__ void corr_bwd_tile(float* sm, const float* __restrict
       __syncthreads();  // stage st landed; partial slices free
     }
     USF_TRACE_AT(3 + 5 * st);
-    if (USF_BWD_PRIO == 2) __builtin_amdgcn_s_setprio(2);
     if (st + NB - 1 < nst) dma_stage(cbeg + (st + NB - 1) * CC, sm + wr * XIMG);
-    if (USF_BWD_PRIO == 2) __builtin_amdgcn_s_setprio(0);
     const float* cur = sm + rd * XIMG;
     USF_TRACE_AT(4 + 5 * st);
-    if (USF_BWD_PRIO == 1) __builtin_amdgcn_s_setprio(2);
     bwd_stage<D, PX, SEGX, NW, CC, V, G2>(gv, cur, red + wave * (CC * TH * TW) + lane * PX, wave, r, q, ep);
-    if (USF_BWD_PRIO == 1) __builtin_amdgcn_s_setprio(0);
     USF_TRACE_AT(5 + 5 * st);
     if (!TOPWAIT) dma_wait_all();  // stage st + 1 (NB == 2: nothing else in flight)
     USF_TRACE_AT(6 + 5 * st);

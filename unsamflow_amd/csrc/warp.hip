@@ -429,7 +429,9 @@ __global__ __launch_bounds__(256) void warp_bwd_kernel(const float* __restrict__
       }
     }
   }
-  if (BIN == 2 && t == 0) ba.hdr[1] = at_use(par);  // handed to the gather, which flips hdr[0] for the next call
+  // handed to the gather, which flips hdr[0] for the next call (one writer: a
+  // same-address store from every workgroup would queue on one L2 line)
+  if (BIN == 2 && t == 0 && linear_block() == 0) ba.hdr[1] = at_use(par);
   // grad_x: reduce-by-key over the wave per corner row (see scatter_row)
   RowRuns rn{}, rs{};
   if (WANT_GX) {
