@@ -230,19 +230,28 @@ def copy_ceiling_gbps(device, mib=512, reps=10):
 
 
 def pmc_traffic(op, shape):
-    """HBM bytes per launch of (op, shape) from the newest committed PMC summary."""
+    """HBM bytes per launch of (op, shape) from the newest committed PMC summary
+    (profiles/*_pmc_traffic.json, tools/pmc_traffic.py) measured on THIS build:
+    a summary whose build_id differs from the loaded library's usf_build_id is
+    never used -- a changed kernel must not inherit an old figure.
+    Returns (bytes or None, source file or None, note)."""
+    from unsamflow_amd import _lib
+
     def natural(path):  # r01_v12 after r01_v9
         return [int(t) if t.isdigit() else t for t in re.split(r"(\d+)", os.path.basename(path))]
 
+    bid = _lib.build_id()
     files = sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_traffic.json")), key=natural)
-    if not files:
-        return None, None
-    with open(files[-1]) as f:
-        data = json.load(f)
-    for site in data.get("sites", []):
-        if site["op"] == op and list(site["shape"]) == list(shape):
-            return site["traffic_bytes"], os.path.relpath(files[-1], REPO)
-    return None, None
+    for path in reversed(files):
+        with open(path) as f:
+            data = json.load(f)
+        if data.get("build_id") != bid:
+            continue
+        for site in data.get("sites", []):
+            if site["op"] == op and list(site["shape"]) == list(shape):
+                return site["traffic_bytes"], os.path.relpath(path, REPO), f"build {bid}"
+        return None, os.path.relpath(path, REPO), f"build {bid}: the summary does not cover this site"
+    return None, None, f"no committed PMC summary of build {bid} (profiles/*_pmc_traffic.json)"
 
 
 def survey_configs_gpu(device):
@@ -491,6 +500,8 @@ def main():
     # eager: two event records per hot-path launch inside the timed region (no syncs);
     # graph replays carry no host code, so their per-site times come from the
     # in-step pass below
+    if on_gpu and not use_graph:
+        step.phase_events = []  # (start, after backward, end) device events per timed step
     with KernelTimer(enabled=on_gpu and not use_graph) as kt:
         t0 = time.perf_counter()
         for _ in range(args.steps):
@@ -508,10 +519,21 @@ def main():
             for _ in range(args.steps):
                 step(img1, img2, s1, s2)
             sync()
+    phases = None
+    if step.phase_events:
+        # fwd(with_bk) + unFlowLoss + backward, and the optimizer
+        # step (clip_grad_norm_ + Adam + OneCycleLR) reported apart; device time
+        # between events recorded on the step's stream (max over ranks below)
+        fb = sum(e[0].elapsed_time(e[1]) for e in step.phase_events) / len(step.phase_events)
+        op = sum(e[1].elapsed_time(e[2]) for e in step.phase_events) / len(step.phase_events)
+        step.phase_events = None
+        phases = [fb, op]
     if distributed:
-        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        t = torch.tensor([elapsed] + (phases or [0.0, 0.0]), device=device, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = t.item()
+        elapsed = t[0].item()
+        if phases:
+            phases = [t[1].item(), t[2].item()]
     loss_val = float(loss.item())
 
     rows = roof = per_op_us = gpu_configs = None
@@ -520,9 +542,10 @@ def main():
         rows, roof, per_op_us = kernel_report(summary, device, args.steps, replay=not args.no_replay)
         roof["copy_ceiling_gbps"] = copy_ceiling_gbps(device)
         roof["frac_of_copy"] = round(roof["achieved"] / roof["copy_ceiling_gbps"], 4)
-        traffic, src = pmc_traffic(roof["kernel"], roof["shape"])
+        traffic, src, note = pmc_traffic(roof["kernel"], roof["shape"])
         roof["traffic"] = traffic
         roof["traffic_source"] = src
+        roof["traffic_note"] = note
         gpu_configs = None if args.no_replay else survey_configs_gpu(device)
 
     cpu = None
@@ -556,6 +579,14 @@ def main():
                 "parallelism": f"dp{world}",
             },
             "final_loss": round(loss_val, 6),
+            # the step split as BASELINE.md 4 defines the metric: fwd + loss + bwd, and
+            # the optimizer step (clip + Adam + scheduler) apart. ms_per_step and value
+            # stay the all-in wall time of the timed region (the driver's clock)
+            "phases": None if not phases else {
+                "fwd_loss_bwd_ms": round(phases[0], 3), "optimizer_ms": round(phases[1], 3),
+                "pairs_per_s_fwd_loss_bwd": round(args.batch * world / (phases[0] / 1e3), 3),
+                "method": "HIP events on the step stream around fwd+loss+bwd and clip+Adam+OneCycleLR, "
+                          "mean over the timed steps, max over ranks"},
             # per call site, one compact row each (the driver keeps the last 8 KB of
             # stdout, so the summaries below come after this list)
             "levels_fields": LEVEL_FIELDS,

@@ -68,12 +68,13 @@
 extern "C" {
 #endif
 
-#define USF_ABI_VERSION 7
+#define USF_ABI_VERSION 8
 #define USF_EINVAL (-1)
 #define USF_EDEVICE (-2) /* a kernel raised a device error flag (USF_SYNC_CHECK=1 only) */
 
 /* device error flags (usf_device_errors) */
 #define USF_DEVERR_WARP_OVERFLOW 1 /* binned warp backward: overflow list past its capacity */
+#define USF_DEVERR_WORKSPACE_DIRTY 2 /* a *_persist_* workspace not left reusable (USF_SYNC_CHECK=1) */
 
 /* padding modes for the warp (flow_warp `pad` argument) */
 #define USF_PAD_ZEROS 0
@@ -81,6 +82,12 @@ extern "C" {
 
 /* ABI version of the loaded library (== USF_ABI_VERSION it was built with). */
 int usf_abi_version(void);
+
+/* Identity of this build: 16 hex digits of a sha256 over the library's
+ * sources, headers and compiler flags (unsamflow_amd/build.py build_id).
+ * Measurement summaries (PMC traffic) carry it, so a figure is only ever
+ * attributed to the build it was measured on. */
+const char* usf_build_id(void);
 
 /* Human-readable description of the last error on the calling thread
  * ("" if none). The pointer stays valid until the next call on this thread. */

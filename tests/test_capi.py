@@ -30,7 +30,7 @@ def declared_symbols():
 def test_header_declares_the_abi():
     syms = declared_symbols()
     assert syms == sorted(
-        ["usf_abi_version", "usf_last_error_string", "usf_corr_fwd_f32", "usf_corr_bwd_f32",
+        ["usf_abi_version", "usf_build_id", "usf_last_error_string", "usf_corr_fwd_f32", "usf_corr_bwd_f32",
          "usf_corr_fwd_ex_f32", "usf_corr_fwd_workspace", "usf_corr_bwd_ex_f32", "usf_corr_act_mask_words",
          "usf_corr_bwd_ex_scratch",
          "usf_warp_fwd_f32", "usf_warp_bwd_f32", "usf_warp_bwd_ex_f32", "usf_warp_bwd_workspace",
@@ -57,10 +57,20 @@ def test_library_exports_every_declared_symbol(lib):
     assert set(_lib.EXPORTED_SYMBOLS) == set(declared_symbols())
 
 
+def test_build_id_matches_the_tree(lib):
+    """The library carries the id of the sources it was built from, so a
+    measurement summary can be matched to the build it was taken on."""
+    from unsamflow_amd import _lib
+    from unsamflow_amd.build import build_id
+
+    assert _lib.build_id() == build_id()
+    assert re.fullmatch(r"[0-9a-f]{16}", _lib.build_id())
+
+
 def test_abi_version(lib):
     from unsamflow_amd import _lib
 
-    assert lib.usf_abi_version() == _lib.ABI_VERSION == 7
+    assert lib.usf_abi_version() == _lib.ABI_VERSION == 8
 
 
 def test_no_torch_types_in_abi():

@@ -115,6 +115,6 @@ def test_occ_persist_call_sequence_matches_per_call_form(hip_device):
                 _lib.check(rc, "usf_splat_map_f32")
                 assert bool(((m[diff].clamp(0, 1) - 0.2).abs() < 1e-5).all()), (B, H, W, kind)
     torch.cuda.synchronize()
-    for key, ws in ops._PERSIST.items():
+    for key, (ws, _) in ops._PERSIST.items():
         if key[1] == "occ_bwd":
             assert int(torch.count_nonzero(ws)) == 0, key  # the threshold pass left every map zero

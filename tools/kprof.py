@@ -41,7 +41,15 @@ def selected_sites():
     return [s for s in SITES if not only or s[0] in only.split(",")]
 
 
+SEPARATOR = "stream_copy_kernel"  # the marker kernel between launches (usf_stream_copy_f32 of 4 floats)
+
+
 def main():
+    """Per site: its launcher (setup kernels), then n x (separator, launch),
+    then a closing separator. tools/pmc_traffic.py cuts the dispatch list at
+    the separators, so every launch's kernels -- however many one call runs
+    (persistent two-launch forms, split forwards, fills) -- are summed as that
+    launch, and the setup kernels fall outside every launch."""
     lib = _lib.load()
     if os.environ.get("USF_PHOTO_VARIANT"):  # usf_set_variant op 3: one pair kernel, only -1 / 0 accepted
         v = int(os.environ["USF_PHOTO_VARIANT"])
@@ -54,15 +62,19 @@ def main():
     b = torch.empty_like(a)
     for _ in range(n):
         b.copy_(a)
-    # KPROF_BWD_VARIANTS="-1,4": every site once per correlation-backward variant (usf_set_variant(1, v))
-    for v in [int(t) for t in os.environ.get("KPROF_BWD_VARIANTS", "-1").split(",")]:
-        lib.usf_set_variant(1, v)
-        for op, key in selected_sites():
-            fn = site_launcher(op, key, dev)
-            for _ in range(n):
-                fn()
-            torch.cuda.synchronize()
-    lib.usf_set_variant(1, -1)
+    sa, sb = torch.zeros(4, device=dev), torch.empty(4, device=dev)
+    stream = _lib.stream_handle(dev)
+
+    def sep():
+        _lib.check(lib.usf_stream_copy_f32(sa.data_ptr(), sb.data_ptr(), 4, stream), "usf_stream_copy_f32")
+
+    for op, key in selected_sites():
+        fn = site_launcher(op, key, dev)
+        for _ in range(n):
+            sep()
+            fn()
+        sep()
+        torch.cuda.synchronize()
     print("kprof done")
 
 

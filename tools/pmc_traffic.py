@@ -3,9 +3,11 @@
 Input: the FETCH_SIZE and WRITE_SIZE passes of tools/gpu_pmc.sh over
 tools/kprof.py (each its own rocprofv3 --pmc run with --kernel-trace only).
 kprof.py launches, in order: a 256 MiB device copy (n times, calibration),
-then every site of kprof.SITES n times; each site launch contains exactly one
-usf:: kernel (two for occ_bwd and photo_fwd[_grad]), so usf dispatches map to sites
-by order.
+then every site of kprof.SITES n times, each launch behind a separator kernel
+(kprof.SEPARATOR); the usf:: dispatches between two separators are one launch,
+however many kernels it runs. The summary carries the library's build id
+(usf_build_id): bench.py only takes a traffic figure measured on the build it
+has loaded.
 
 Correction (MI355X_MICROARCH.md, HBM/rocprofv3): FETCH_SIZE under-reports
 wide streaming reads by 2x on gfx950 and other access widths are uncalibrated,
@@ -40,9 +42,32 @@ def per_dispatch(path, counter):
     return [d[k] for k in sorted(d)]
 
 
+def launches(rows, nsites, n):
+    """Cut the dispatch list at the separator kernels (tools/kprof.py): per
+    site n launches, each the list of (kernel, value) of its usf:: kernels."""
+    from kprof import SEPARATOR
+
+    seps = [i for i, (name, _) in enumerate(rows) if SEPARATOR in name]
+    if len(seps) != nsites * (n + 1):
+        raise SystemExit(f"expected {nsites * (n + 1)} separator dispatches, found {len(seps)}")
+    out = []
+    for s in range(nsites):
+        base = s * (n + 1)
+        out.append([[(name, v) for name, v in rows[seps[base + j] + 1:seps[base + j + 1]] if "usf::" in name]
+                    for j in range(n)])
+    return out
+
+
+def short(name):
+    """Kernel name without namespaces and argument lists."""
+    base = name.split("(")[0]
+    return base.replace("usf::(anonymous namespace)::", "").replace("usf::", "")
+
+
 def main():
     root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc"
     from kprof import selected_sites
+    from unsamflow_amd import _lib
     from unsamflow_amd.kernel_timer import corr_bytes, warp_bytes
 
     n = int(os.environ.get("KPROF_N", "3"))
@@ -50,37 +75,25 @@ def main():
     write = per_dispatch(f"{root}/p4/run_counter_collection.csv", "WRITE_SIZE")
 
     def calib(rows):
-        copies = [v for name, v in rows if "copy" in name.lower()][:n]
+        from kprof import SEPARATOR
+
+        copies = [v for name, v in rows if "copy" in name.lower() and SEPARATOR not in name][:n]
         return COPY_BYTES / (statistics.median(copies) * 1024)
 
     f_read, f_write = calib(fetch), calib(write)
-    uf = [v for name, v in fetch if "usf::" in name]
-    uw = [v for name, v in write if "usf::" in name]
-    # library kernels per launch of a site (summed): zero fill + splat + threshold, partials + final
-    per_launch = {"occ_bwd": 3, "photo_fwd": 2, "photo_fwd_grad": 2, "photo_pair_grad": 2, "corr_bwd_leaky": 2,
-                  "convex_up_bwd": 2}
-    # kernels a site's launcher runs once before its timed launches
-    prefix = {}
-    sites, pos = [], 0
-    from unsamflow_amd import _lib
-
-    lib = _lib.load()  # host-only query: split forwards run a second (reduce) kernel
-    for op, key in selected_sites():
-        k = per_launch.get(op, 1)
-        split = lib.usf_corr_fwd_workspace(*key[:4], 4) > 0 if op.startswith("corr") else False
-        if op in ("corr_fwd", "corr_fwd_leaky") and split:
-            k = 2
-        pos += prefix.get(op, 0)
-        if op == "corr_bwd_leaky":
-            # sign-mask path at every level: one backward kernel per launch, after
-            # the launcher's forward (two kernels where the forward is split)
-            k = 1
-            pos += 2 if split else 1
-        if op == "warp_bwd" and key[5]:
-            k = 4  # binned grad_x: zero fill, filing (+ grad_flow), gather, overflow
-        fk = statistics.median(sum(uf[pos + j * k + i] for i in range(k)) for j in range(n))
-        wk = statistics.median(sum(uw[pos + j * k + i] for i in range(k)) for j in range(n))
-        pos += k * n
+    sites_list = selected_sites()
+    lf, lw = launches(fetch, len(sites_list), n), launches(write, len(sites_list), n)
+    lib = _lib.load()  # host-only queries (no GPU work)
+    sites = []
+    for (op, key), fl, wl in zip(sites_list, lf, lw):
+        fk = statistics.median(sum(v for _, v in launch) for launch in fl)
+        wk = statistics.median(sum(v for _, v in launch) for launch in wl)
+        # per kernel of the launch (median over the launches), in launch order
+        names = [short(k) for k, _ in fl[0]]
+        per_kernel = [{"kernel": nm,
+                       "fetch_kib": round(statistics.median(launch[i][1] for launch in fl if len(launch) > i), 1),
+                       "write_kib": round(statistics.median(launch[i][1] for launch in wl if len(launch) > i), 1)}
+                      for i, nm in enumerate(names)]
         if op == "photo_bwd":
             B, ndir, H, W = key
         elif op.startswith("convex_up"):
@@ -118,12 +131,13 @@ def main():
         row = {"op": op, "shape": list(key), "fetch_kib": round(fk, 1), "write_kib": round(wk, 1),
                "read_bytes": int(fk * 1024 * f_read), "write_bytes": int(wk * 1024 * f_write),
                "traffic_bytes": int(traffic), "algorithmic_bytes": int(alg),
-               "traffic_over_algorithmic": round(traffic / alg, 3)}
+               "traffic_over_algorithmic": round(traffic / alg, 3), "kernels": per_kernel}
         if op == "photo_pair_grad":  # reads against the read-once minimum (48 B/px at C = 3)
             row["read_once_bytes"] = 4 * B * H * W * (2 * C + 4 + 2)
             row["read_over_read_once"] = round(row["read_bytes"] / row["read_once_bytes"], 3)
         sites.append(row)
-    print(json.dumps({"calibration": {"copy_bytes": COPY_BYTES, "fetch_scale": round(f_read, 4),
+    print(json.dumps({"build_id": lib.usf_build_id().decode(),
+                      "calibration": {"copy_bytes": COPY_BYTES, "fetch_scale": round(f_read, 4),
                                       "write_scale": round(f_write, 4), "launches_per_site": n},
                       "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes, --kernel-trace only) "
                                 "over tools/kprof.py, scaled by a 256 MiB copy calibration",

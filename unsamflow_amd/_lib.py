@@ -17,7 +17,7 @@ from pathlib import Path
 import torch  # noqa: F401  (load torch's HIP runtime before the plugin)
 
 _LIB_PATH = Path(os.environ.get("USF_LIB", Path(__file__).resolve().parent / "lib" / "libunsamflow_hip.so"))
-ABI_VERSION = 7
+ABI_VERSION = 8
 PAD_ZEROS = 0
 PAD_BORDER = 1
 
@@ -26,6 +26,7 @@ _c_float_p = ctypes.c_void_p
 _SIGNATURES = {
     "usf_abi_version": ([], ctypes.c_int),
     "usf_last_error_string": ([], ctypes.c_char_p),
+    "usf_build_id": ([], ctypes.c_char_p),
     "usf_corr_fwd_f32": (
         [_c_float_p, _c_float_p, _c_float_p] + [ctypes.c_int] * 5 + [ctypes.c_void_p],
         ctypes.c_int,
@@ -154,6 +155,11 @@ def load() -> ctypes.CDLL:
             raise RuntimeError(f"libunsamflow_hip.so ABI version {v} != expected {ABI_VERSION}")
         _lib = lib
         return lib
+
+
+def build_id() -> str:
+    """The loaded library's build id (usf_build_id; unsamflow_amd.build.build_id)."""
+    return load().usf_build_id().decode()
 
 
 def is_available() -> bool:

@@ -9,6 +9,7 @@ Usage: ``python -m unsamflow_amd.build [--force] [--verbose]``
 from __future__ import annotations
 
 import argparse
+import hashlib
 import os
 import subprocess
 import sys
@@ -47,6 +48,20 @@ COMMON_FLAGS = [
 ]
 
 
+def build_id() -> str:
+    """Identity of the library this tree builds: sha256 (16 hex digits) over
+    every source and header text, the compiler flags and the target. It is
+    compiled into the library (usf_build_id) and stamped into the PMC
+    summaries (tools/pmc_traffic.py), so bench.py never reports a traffic
+    figure measured on another build."""
+    h = hashlib.sha256()
+    for f in [CSRC / s for s in SOURCES] + [CSRC / s for s in HEADERS] + [INCLUDE_DIR / "unsamflow_hip.h"]:
+        h.update(f.name.encode())
+        h.update(f.read_bytes())
+    h.update(" ".join(COMMON_FLAGS).encode())
+    return h.hexdigest()[:16]
+
+
 def _stale(target: Path, deps: list[Path]) -> bool:
     if not target.exists():
         return True
@@ -64,15 +79,21 @@ def build_library(force: bool = False, verbose: bool = False) -> Path:
     obj_dir = LIB_DIR / "obj"
     obj_dir.mkdir(exist_ok=True)
     headers = [CSRC / h for h in HEADERS] + [INCLUDE_DIR / "unsamflow_hip.h"]
+    bid = build_id()
+    stamp = obj_dir / "build_id.txt"
+    id_changed = not stamp.exists() or stamp.read_text().strip() != bid
     objs = []
     for src in SOURCES:
         s = CSRC / src
         o = obj_dir / (s.stem + ".o")
         objs.append(o)
-        if force or _stale(o, [s] + headers):
+        # capi.cpp carries the build id: rebuilt whenever any source changed
+        if force or _stale(o, [s] + headers) or (src == "capi.cpp" and id_changed):
             lang = ["-x", "hip"] if src.endswith(".hip") else []
-            cmd = [HIPCC, *COMMON_FLAGS, *lang, "-c", str(s), "-o", str(o)]
+            extra = [f'-DUSF_BUILD_ID="{bid}"'] if src == "capi.cpp" else []
+            cmd = [HIPCC, *COMMON_FLAGS, *extra, *lang, "-c", str(s), "-o", str(o)]
             _run(cmd, verbose)
+    stamp.write_text(bid + "\n")
     if force or _stale(LIB_PATH, objs):
         tmp = LIB_PATH.with_suffix(".so.tmp")
         cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, objs), "-o", str(tmp)]

@@ -50,10 +50,19 @@ static bool sync_check() {
   return on;
 }
 
+// A stream under graph capture cannot be synchronised: the debug checks skip it
+// (the replays of the graph run the same kernels unchecked).
+static bool capturing(hipStream_t s) {
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  return hipStreamIsCapturing(s, &st) == hipSuccess && st != hipStreamCaptureStatusNone;
+}
+
+static bool sync_check_on(hipStream_t s) { return sync_check() && !capturing(s); }
+
 // With USF_SYNC_CHECK=1 every entry point first drains the stream, so a fault
 // raised by an EARLIER (non-usf) kernel is reported as such, not blamed on us.
 static int pre_check(const char* fn, hipStream_t s) {
-  if (!sync_check()) return 0;
+  if (!sync_check_on(s)) return 0;
   const hipError_t e = hipStreamSynchronize(s);
   if (e != hipSuccess) {
     fprintf(stderr, "[usf] %s: stream already faulted BEFORE this launch: %s\n", fn, hipGetErrorString(e));
@@ -64,7 +73,7 @@ static int pre_check(const char* fn, hipStream_t s) {
 }
 
 static int finish(const char* fn, hipError_t e, hipStream_t s) {
-  if (e == hipSuccess && sync_check()) {
+  if (e == hipSuccess && sync_check_on(s)) {
     e = hipStreamSynchronize(s);
     if (e != hipSuccess) fprintf(stderr, "[usf] %s: fault after launch: %s\n", fn, hipGetErrorString(e));
     const int flags = e == hipSuccess ? device_errors(s, true) : 0;
@@ -88,6 +97,11 @@ using namespace usf;
 extern "C" {
 
 int usf_abi_version(void) { return USF_ABI_VERSION; }
+
+#ifndef USF_BUILD_ID
+#define USF_BUILD_ID "unstamped"
+#endif
+const char* usf_build_id(void) { return USF_BUILD_ID; }
 
 const char* usf_last_error_string(void) { return g_err; }
 
@@ -286,12 +300,19 @@ static int warp_bwd_common(const char* fn, const float* x, const float* flow, lo
       set_error("%s: C=%d H=%d W=%d beyond the persistent form (C <= 256, H < 32768, W < 65536)", fn, C, H, W);
       return USF_EINVAL;
     }
+    // the gather reads both count buffers through one buffer descriptor with
+    // 32-bit byte offsets: 2 x 4 bytes per cell must stay below 2^31
+    if (8LL * B * (H + 1) * (W + 1) >= (1LL << 31)) {
+      set_error("%s: B=%d H=%d W=%d: 8*B*(H+1)*(W+1) >= 2^31 (count buffers past 32-bit offsets)", fn, B, H, W);
+      return USF_EINVAL;
+    }
   }
   if (const int pe = pre_check(fn, (hipStream_t)stream)) return pe;
-  return finish(fn,
-                warp_bwd_launch(x, flow, flow_bstride, gout, gx, gflow, B, C, H, W, pad_mode,
-                                (hipStream_t)stream, ws, ws_bytes, persist),
-                (hipStream_t)stream);
+  hipError_t e = warp_bwd_launch(x, flow, flow_bstride, gout, gx, gflow, B, C, H, W, pad_mode, (hipStream_t)stream,
+                                 ws, ws_bytes, persist);
+  if (e == hipSuccess && persist && gx && sync_check_on((hipStream_t)stream))
+    e = warp_persist_check_launch(ws, B, C, H, W, (hipStream_t)stream);
+  return finish(fn, e, (hipStream_t)stream);
 }
 
 int usf_warp_bwd_f32(const float* x, const float* flow, long long flow_bstride,
@@ -370,8 +391,10 @@ int usf_occ_backward_persist_f32(const float* flow21, long long flow_bstride, fl
     return USF_EINVAL;
   }
   if (const int pe = pre_check(fn, (hipStream_t)stream)) return pe;
-  return finish(fn, occ_backward_persist_launch(flow21, flow_bstride, occ, map, B, H, W, th, (hipStream_t)stream),
-                (hipStream_t)stream);
+  hipError_t e = occ_backward_persist_launch(flow21, flow_bstride, occ, map, B, H, W, th, (hipStream_t)stream);
+  if (e == hipSuccess && sync_check_on((hipStream_t)stream))
+    e = zero_check_launch(map, 4LL * B * H * W, (hipStream_t)stream);
+  return finish(fn, e, (hipStream_t)stream);
 }
 
 int usf_occ_bidirection_f32(const float* flow12, long long flow12_bstride, const float* flow21,

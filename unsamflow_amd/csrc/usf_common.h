@@ -106,6 +106,12 @@ hipError_t warp_bwd_launch(const float* x, const float* flow, long long flow_bst
 long long warp_bwd_workspace(int B, int H, int W);
 // bytes of the persistent workspace of usf_warp_bwd_persist_f32
 long long warp_bwd_persist_workspace(int B, int C, int H, int W);
+// USF_SYNC_CHECK only: raise USF_DEVERR_WORKSPACE_DIRTY unless a persistent
+// workspace is back in the state the next call expects (warp: the next call's
+// count buffer, the dirty words and the overflow buffer all zero; occlusion:
+// the splat map zero)
+hipError_t warp_persist_check_launch(void* ws, int B, int C, int H, int W, hipStream_t s);
+hipError_t zero_check_launch(const void* p, long long bytes, hipStream_t s);
 
 hipError_t splat_launch(const float* flow, long long flow_bstride, float* map, int B, int H, int W,
                         bool absolute, hipStream_t s);

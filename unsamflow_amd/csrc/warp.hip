@@ -1871,6 +1871,51 @@ hipError_t warp_bwd_launch(const float* x, const float* flow, long long fbs, con
   return hipGetLastError();
 }
 
+namespace {
+// Persistent-workspace audit (USF_SYNC_CHECK=1 only, after the call's own
+// launches): any nonzero word where the next call expects zero raises
+// USF_DEVERR_WORKSPACE_DIRTY, so a faulted or interrupted call cannot
+// silently poison the calls of that shape that follow.
+__global__ __launch_bounds__(256) void zero_check_kernel(const unsigned* __restrict__ p, long long n) {
+  bool bad = false;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256)
+    bad |= p[i] != 0u;
+  if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(&g_dev_errors, USF_DEVERR_WORKSPACE_DIRTY);
+}
+// the warp backward's next count buffer is the one the parity word selects
+__global__ __launch_bounds__(256) void cnt_check_kernel(const int* __restrict__ hdr, const unsigned* __restrict__ cnt2,
+                                                        long long ncell) {
+  const int par = hdr[0];
+  bool bad = par != 0 && par != 1;
+  const unsigned* c = cnt2 + (size_t)(par & 1) * ncell;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < ncell; i += (long long)gridDim.x * 256)
+    bad |= c[i] != 0u;
+  if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(&g_dev_errors, USF_DEVERR_WORKSPACE_DIRTY);
+}
+}  // namespace
+
+hipError_t zero_check_launch(const void* p, long long bytes, hipStream_t s) {
+  const long long n = bytes / 4;
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(zero_check_kernel, dim3((unsigned)std::min<long long>((n + 255) / 256, 2048)), dim3(256), 0,
+                     s, static_cast<const unsigned*>(p), n);
+  return hipGetLastError();
+}
+
+hipError_t warp_persist_check_launch(void* ws, int B, int C, int H, int W, hipStream_t s) {
+  const BinLayout2 L = bin_layout2(B, C, H, W);
+  const GatherGrid gg = gather_grid(B, C, H, W);
+  char* w = static_cast<char*>(ws);
+  const long long ncell = (long long)B * (H + 1) * (W + 1);
+  hipLaunchKernelGGL(cnt_check_kernel, dim3((unsigned)std::min<long long>((ncell + 255) / 256, 2048)), dim3(256),
+                     0, s, reinterpret_cast<const int*>(w + L.hdr_off),
+                     reinterpret_cast<const unsigned*>(w + L.cnt_off), ncell);
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess) e = zero_check_launch(w + L.dirty_off, 4LL * B * gg.ntiles, s);
+  if (e == hipSuccess) e = zero_check_launch(w + L.ovfgx_off, 4LL * B * C * H * W, s);
+  return e;
+}
+
 long long warp_bwd_workspace(int B, int H, int W) { return bin_layout(B, H, W).total; }
 long long warp_bwd_persist_workspace(int B, int C, int H, int W) { return bin_layout2(B, C, H, W).total; }
 

@@ -92,6 +92,10 @@ class TrainStep:
         else:
             self.scheduler = torch.optim.lr_scheduler.ExponentialLR(self.optimizer, gamma=1)
         self.max_grad_norm = t.max_grad_norm
+        # None, or a list that every call appends one (start, after backward, end)
+        # triple of device events to: the optimizer step (clip + Adam + scheduler)
+        # timed apart from fwd + loss + bwd (bench.py)
+        self.phase_events: list | None = None
 
     def forward_loss(self, img1, img2, full_seg1=None, full_seg2=None):
         res = self.model(img1, img2, full_seg1, full_seg2, with_bk=True)
@@ -103,12 +107,21 @@ class TrainStep:
         return loss.mean(), flows
 
     def __call__(self, img1, img2, full_seg1=None, full_seg2=None):
+        ev = None
+        if self.phase_events is not None:
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+            ev[0].record()
         loss, _ = self.forward_loss(img1, img2, full_seg1, full_seg2)
         self.optimizer.zero_grad(set_to_none=True)
         loss.backward()
+        if ev is not None:
+            ev[1].record()
         torch.nn.utils.clip_grad_norm_(self.model.parameters(), self.max_grad_norm)
         self.optimizer.step()
         self.scheduler.step()
+        if ev is not None:
+            ev[2].record()
+            self.phase_events.append(ev)
         return loss.detach()
 
 

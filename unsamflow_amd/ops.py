@@ -9,6 +9,8 @@ from __future__ import annotations
 
 import torch
 
+from collections import OrderedDict
+
 from . import _lib
 from . import kernel_timer as _kt
 
@@ -168,25 +170,59 @@ def warp_forward(x: torch.Tensor, flow: torch.Tensor, pad: str = "border") -> to
 
 
 # Persistent workspaces of the *_persist_* entry points (include/unsamflow_hip.h,
-# ABI 7): zeroed once when created, then left reusable by every call, so the
-# per-call fill launch is gone. One per (device, op, shape). Calls of one op and
-# shape must not overlap on two streams at once: this package issues every call
-# on torch's current stream, and its graph captures (kernel_timer, harness) warm
-# up on a side stream that the capture stream waits for -- so the capture reuses
-# the eager workspace and records no fill.
-_PERSIST: dict = {}
+# ABI 8): zeroed once when created, then left reusable by every call, so the
+# per-call fill launch is gone. One per (device, op, shape). The state they
+# carry (a parity word, count buffers, dirty words, an overflow buffer, the
+# occlusion splat map) must see its calls in order, so each entry records the
+# stream of its last eager use, and a call from another stream first makes its
+# stream wait for that one (torch's wait_stream): two streams can never race a
+# workspace. A HIP graph capture reuses the workspace its eager warm-up created
+# (torch captures on its own stream; the capture records no fill, and replays
+# are uses on the replaying stream). The cache is bounded (least recently used
+# out): each warp entry holds ~88 B per pixel plus one float per element of x,
+# each occlusion entry 4 B per pixel, and a training run with a changing shape
+# (a partial last batch, evaluation at another resolution) must not keep every
+# shape's buffers alive. A call that fails drops its entry (its state may be
+# half-updated): the next call of that shape starts from a fresh zeroed buffer.
+_PERSIST: "OrderedDict[tuple, list]" = OrderedDict()
+PERSIST_MAX_ENTRIES = 32
 
 
 def persistent_workspace(device: torch.device, op: str, shape: tuple, nbytes: int) -> torch.Tensor:
     """The zero-initialised persistent workspace of ``op`` at ``shape`` on
-    ``device`` (created on first use with torch.zeros on the current stream, so
-    the zeroing is ordered before the first call)."""
-    key = (device.index, op, shape)
-    ws = _PERSIST.get(key)
-    if ws is None or ws.numel() < nbytes:
-        ws = torch.zeros(nbytes, device=device, dtype=torch.uint8)
-        _PERSIST[key] = ws
+    ``device``, ordered after its previous use (created on first use with
+    torch.zeros on the current stream, so the zeroing precedes the first call)."""
+    key = (device.index, op, tuple(shape))
+    cur = torch.cuda.current_stream(device)
+    capturing = torch.cuda.is_current_stream_capturing()
+    ent = _PERSIST.get(key)
+    if ent is not None and ent[0].numel() >= nbytes:
+        _PERSIST.move_to_end(key)
+        if not capturing:
+            if ent[1] != cur:
+                cur.wait_stream(ent[1])  # the previous use on another stream comes first
+            ent[1] = cur
+        return ent[0]
+    if capturing:
+        # torch.zeros inside a capture is only recorded: the eager calls after it
+        # would start from uninitialised state
+        raise RuntimeError(
+            f"unsamflow_amd: first use of the persistent {op} workspace for shape {tuple(shape)} inside a "
+            "HIP graph capture; run the call once eagerly before capturing")
+    ws = torch.zeros(nbytes, device=device, dtype=torch.uint8)
+    _PERSIST[key] = [ws, cur]
+    while len(_PERSIST) > PERSIST_MAX_ENTRIES:
+        _PERSIST.popitem(last=False)
     return ws
+
+
+def _drop_workspace(device: torch.device, op: str, shape: tuple) -> None:
+    _PERSIST.pop((device.index, op, tuple(shape)), None)
+
+
+def clear_persistent_workspaces() -> None:
+    """Release every persistent workspace (the next call of each shape re-creates it)."""
+    _PERSIST.clear()
 
 
 def warp_backward(
@@ -205,8 +241,8 @@ def warp_backward(
     order, so grad_x is deterministic unless a cell receives more than 4 source
     pixels (strongly compressive flow), whose excess is added with fp32
     atomics. Its workspace (``usf_warp_bwd_persist_workspace``: ~88 B per pixel
-    plus one float per element of x) is kept per stream and shape
-    (:func:`persistent_workspace`). grad_flow is deterministic."""
+    plus one float per element of x) is kept per (device, shape) and ordered
+    across streams (:func:`persistent_workspace`). grad_flow is deterministic."""
     _require_device_f32("x", x)
     _require_device_f32("flow12", flow)
     _require_device_f32("grad_output", grad_out)
@@ -225,7 +261,9 @@ def warp_backward(
     lib = _lib.load()
     # grad_x by the binned gather, persistent two-launch form (C <= 256), else the
     # four-launch form with a per-call workspace from torch's caching allocator
-    persist = need_x and C <= 256 and H < 32768 and W < 65536
+    # (the C ABI's limits of the persistent form: a 32-bit dirty mask of channel
+    # groups, packed (y, x), both count buffers under 32-bit byte offsets)
+    persist = need_x and C <= 256 and H < 32768 and W < 65536 and 8 * B * (H + 1) * (W + 1) < 2 ** 31
     with torch.cuda.device(x.device):
         if persist:
             nws = int(lib.usf_warp_bwd_persist_workspace(B, C, H, W))
@@ -238,6 +276,8 @@ def warp_backward(
                        _kt.warp_bytes(B, C, H, W, True, need_x, need_flow)):
             rc = fn(xc.data_ptr(), fv.data_ptr(), fbs, gc.data_ptr(), _ptr(gx), _ptr(gf), _ptr(ws), nws,
                     B, C, H, W, PAD_MODES[pad], _lib.stream_handle(x.device))
+    if rc != 0 and persist:
+        _drop_workspace(x.device, "warp_bwd", (B, C, H, W))
     _lib.check(rc, "usf_warp_bwd_persist_f32" if persist else "usf_warp_bwd_ex_f32")
     return gx, gf
 
@@ -280,6 +320,8 @@ def occ_backward(flow21: torch.Tensor, th: float = 0.2) -> torch.Tensor:
         with _kt.timed("occ_bwd", (B, 1, H, W), flow21.device, 4 * B * H * W * 3):
             rc = lib.usf_occ_backward_persist_f32(fv.data_ptr(), fbs, out.data_ptr(), ws.data_ptr(), nmap, B, H, W,
                                                   float(th), _lib.stream_handle(flow21.device))
+    if rc != 0:
+        _drop_workspace(flow21.device, "occ_bwd", (B, H, W))
     _lib.check(rc, "usf_occ_backward_persist_f32")
     return out
 
