@@ -167,11 +167,7 @@ int usf_warp_fwd_f32(const float* x, const float* flow, long long flow_bstride,
 
 /* Backward of usf_warp_fwd_f32. gout: [B,C,H,W] dense.
  * gx: [B,C,H,W] or NULL; overwritten (the library zeroes it, then scatters
- *     with fp32 atomics: summation order not fixed). Variant 4 of
- *     usf_set_variant(2, .) gathers instead for sources with |flow| < 2 px.
- *     Variant 7 (images of at most 256 pixels, H, W >= 2; here and in
- *     usf_warp_bwd_ex_f32) is a one-launch small-image form: each target cell
- *     sums its sources in pixel order, deterministic, no atomics, no workspace.
+ *     with fp32 atomics: summation order not fixed).
  * gflow: [B,2,H,W] dense or NULL; overwritten, deterministic. */
 int usf_warp_bwd_f32(const float* x, const float* flow, long long flow_bstride,
                      const float* gout, float* gx, float* gflow,
@@ -345,11 +341,8 @@ int usf_stream_copy_f32(const float* src, float* dst, long long n, void* stream)
 /* Tuning hook (benchmarking only; not needed for correct use).
  * Forces kernel variant `index` of `op` for d=4 launches in this process:
  * op 0 = correlation forward tile config, op 1 = correlation backward tile
- * config, op 2 = warp grad_x scatter (0 = wave reduce-by-key + direct global
- * atomics, 1 = LDS-aggregated tiles, 2 / 3 = variant 0 with 4 / 1 channel
- * slices per workgroup, 4 = gather for |flow| < 2 px + scatter for the rest,
- * 5 = scatter over vertically adjacent pixel pairs, 6 = the binned gather
- * (needs the workspace), 7 = the small-image kernel where H*W <= 256), op 3 = photometric
+ * config, op 2 = warp grad_x path (0 = the lane-merged per-pixel scatter, 1 =
+ * the pixel-pair scatter, 2 = the binned gather, which needs a workspace), op 3 = photometric
  * loss kernel (one variant: 0 = row-streaming strips on producer / consumer wave
  * pairs; the tile and one-wave strip kernels were removed); index -1 restores the built-in choice. Returns the number of
  * variants of `op` (so index range is [0, n)), or USF_EINVAL for an unknown op

@@ -111,6 +111,8 @@ def test_no_torch_types_in_abi():
         (lambda L: L.usf_occ_backward_persist_f32(1, 32, 16, 16, 64, 1, 4, 4, 0.2, None), "separate buffer"),
         (lambda L: L.usf_warp_bwd_persist_f32(1, 1, 32, 1, 1, 1, 16, 64, 1, 3, 4, 4, 1, None), "persistent workspace"),
         (lambda L: L.usf_warp_bwd_persist_f32(1, 1, 32, 1, 1, 1, 16, 1 << 40, 1, 300, 4, 4, 1, None), "C=300"),
+        # both count buffers of the persistent form must stay under 32-bit byte offsets
+        (lambda L: L.usf_warp_bwd_persist_f32(1, 1, 8192, 1, 16, 1, 16, 1 << 60, 70000, 4, 64, 64, 1, None), "2^31"),
         (lambda L: L.usf_photo_loss_fwd_f32(1, 1, 1, 1, 32, 1, 1, None, 1, 4, 4, 4, 1, 0.15, 0.85, None), "> 3"),
         (lambda L: L.usf_photo_loss_fwd_f32(1, 1, 1, 1, 32, 1, 1, 1, 1, 3, 4, 4, 9, 0.15, 0.85, None), "pad_mode 9"),
         (lambda L: L.usf_photo_loss_fwd_f32(1, None, 1, 1, 32, 1, 1, None, 1, 3, 4, 4, 1, 0.15, 0.85, None), "null input"),
@@ -151,7 +153,7 @@ def test_variant_override_bounds(lib):
     assert lib.usf_set_variant(4, 0) == -1
     assert lib.usf_set_variant(3, 0) == 1 and lib.usf_set_variant(3, -1) == 1  # photometric: the pair kernel only
     assert lib.usf_set_variant(3, 1) == -1
-    assert lib.usf_set_variant(2, 1) == 8 and lib.usf_set_variant(2, -1) == 8  # warp grad_x: 7 = small image
+    assert lib.usf_set_variant(2, 1) == 3 and lib.usf_set_variant(2, -1) == 3  # warp grad_x: scatter, pairs, bins
     assert lib.usf_set_variant(1, n_bwd - 1) == n_bwd
     assert lib.usf_set_variant(1, -1) == n_bwd
 

@@ -338,12 +338,12 @@ def test_corr_every_tile_variant_vs_oracle(hip_device, shape):
         lib.usf_set_variant(1, -1)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6])
-def test_warp_grad_x_scatter_variants(hip_device, variant):
-    """Every grad_x variant (reduce-by-key atomics with any channel split,
-    LDS-aggregated tiles, the gather with its outlier scatter) matches the
-    oracle, including a large-flow case whose target boxes overflow the LDS
-    budget (and whose sources are mostly gather outliers)."""
+@pytest.mark.parametrize("variant", [0, 1, 2])
+def test_warp_grad_x_variants(hip_device, variant):
+    """Every grad_x path reachable through usf_set_variant(2, .) -- the
+    per-pixel lane-merged scatter, the pixel-pair scatter (the workspace-free
+    entry's defaults) and the binned gather -- matches the oracle, including a
+    large-flow case (many sources per cell: overflow entries)."""
     from unsamflow_amd import _lib, ops
 
     lib = _lib.load()
@@ -545,19 +545,12 @@ def _small_fields(B, H, W, kind):
 @pytest.mark.parametrize("kind", ["zero", "smooth", "collapse", "random"])
 @pytest.mark.parametrize("shape", [(4, 128, 8, 26), (3, 5, 7, 9), (2, 3, 16, 16)])
 def test_warp_backward_small_image_vs_oracle(hip_device, shape, kind, pad):
-    """The small-image backward (usf_set_variant(2, 7), images of <= 256
-    pixels): each target cell sums its sources in pixel order. Matches the
-    oracle for smooth, zero, fully contracting (cells with > 8 sources: the
-    pool path) and large random flows; bit-identical across runs; each
-    gradient alone equals its share of the joint call."""
-    from unsamflow_amd import _lib, ops
-
-    lib = _lib.load()
-    lib.usf_set_variant(2, 7)
-    try:
-        _small_image_case(hip_device, shape, kind, pad)
-    finally:
-        lib.usf_set_variant(2, -1)
+    """The default backward on images of at most 256 pixels (the decoder's
+    level 1 and smaller): matches the oracle for smooth, zero, fully
+    contracting (cells with many sources: overflow entries) and large random
+    flows; bit-identical across runs where no cell overflows (zero, smooth);
+    each gradient alone equals its share of the joint call."""
+    _small_image_case(hip_device, shape, kind, pad)
 
 
 def _small_image_case(hip_device, shape, kind, pad):
@@ -573,27 +566,27 @@ def _small_image_case(hip_device, shape, kind, pad):
     np.testing.assert_allclose(_np(gx), rx, atol=1e-4, rtol=1e-5)
     np.testing.assert_allclose(_np(gf), rf, atol=1e-4, rtol=1e-5)
     gx2, gf2 = ops.warp_backward(tx, tf, tg, pad)
-    assert torch.equal(gx, gx2) and torch.equal(gf, gf2)
+    assert torch.equal(gf, gf2)
+    if kind in ("zero", "smooth"):  # no overflow entries: fixed-order sums only
+        assert torch.equal(gx, gx2)
+    else:
+        torch.testing.assert_close(gx, gx2, atol=1e-5, rtol=1e-5)
     ox, _ = ops.warp_backward(tx, tf, tg, pad, need_flow=False)
     _, of = ops.warp_backward(tx, tf, tg, pad, need_x=False)
-    assert torch.equal(ox, gx) and torch.equal(of, gf)
+    torch.testing.assert_close(ox, gx, atol=1e-5, rtol=1e-5)
+    torch.testing.assert_close(of, gf, atol=1e-5, rtol=1e-5)
 
 
 def test_warp_backward_small_image_flow_slice(hip_device):
-    """The loss-style flow slice (batch stride 4HW) through the small-image kernel."""
-    from unsamflow_amd import _lib, ops
+    """The loss-style flow slice (batch stride 4HW) through the backward at a small image."""
+    from unsamflow_amd import ops
 
     B, C, H, W = 3, 16, 8, 26
     x = hashrng.uniform((B, C, H, W), 740)
     g = hashrng.normal((B, C, H, W), 741)
     f4 = hashrng.symmetric((B, 4, H, W), 742, 2.5)
     t4 = _dev(f4, hip_device)
-    lib = _lib.load()
-    lib.usf_set_variant(2, 7)
-    try:
-        gx, gf = ops.warp_backward(_dev(x, hip_device), t4[:, 2:], _dev(g, hip_device), "border")
-    finally:
-        lib.usf_set_variant(2, -1)
+    gx, gf = ops.warp_backward(_dev(x, hip_device), t4[:, 2:], _dev(g, hip_device), "border")
     rx, rf = warp_backward_np(x, np.ascontiguousarray(f4[:, 2:]), g, "border")
     np.testing.assert_allclose(_np(gx), rx, atol=1e-4, rtol=1e-5)
     np.testing.assert_allclose(_np(gf), rf, atol=1e-4, rtol=1e-5)

@@ -44,7 +44,8 @@ def _ex(x, flow, go, pad):
 
 
 @pytest.mark.parametrize("pad", ["border", "zeros"])
-def test_warp_persist_call_sequence_matches_per_call_form(hip_device, pad):
+def test_warp_persist_call_sequence_matches_per_call_form(hip_device, pad, monkeypatch):
+    monkeypatch.setattr(ops, "WARP_PERSIST_MAX_PIXELS", None)  # the persistent form at every shape
     shapes = [(4, 32, 64, 208), (3, 16, 33, 70)]
     data = {}
     for i, (B, C, H, W) in enumerate(shapes):
@@ -66,10 +67,11 @@ def test_warp_persist_call_sequence_matches_per_call_form(hip_device, pad):
             torch.testing.assert_close(gx, rx, atol=1e-5, rtol=1e-5, msg=lambda m: f"{shapes[si]} {kind}: {m}")
 
 
-def test_warp_persist_workspace_returns_to_reusable_state(hip_device):
+def test_warp_persist_workspace_returns_to_reusable_state(hip_device, monkeypatch):
     """After an overflow-heavy call and a smooth one, the workspace holds no
     leftover: the overflow buffer and every dirty word are zero again, and one
     of the two count buffers is zero (the one the next call files into)."""
+    monkeypatch.setattr(ops, "WARP_PERSIST_MAX_PIXELS", None)
     B, C, H, W = 2, 16, 40, 64
     g = torch.Generator(device=hip_device).manual_seed(31)
     x = torch.randn(B, C, H, W, device=hip_device, generator=g)
@@ -118,3 +120,87 @@ def test_occ_persist_call_sequence_matches_per_call_form(hip_device):
     for key, (ws, _) in ops._PERSIST.items():
         if key[1] == "occ_bwd":
             assert int(torch.count_nonzero(ws)) == 0, key  # the threshold pass left every map zero
+
+
+def _np_fields(B, H, W):
+    """Decoder-style flows as numpy: a smooth +-2 px field with a per-sample
+    phase, a border-piling shift (a strip of sources clamped onto the edge
+    column: many pixels per cell), and a field contracting towards the centre
+    (whole regions share a cell: overflow entries and dirty tiles)."""
+    import numpy as np
+
+    yy, xx = np.meshgrid(np.arange(H, dtype=np.float32), np.arange(W, dtype=np.float32), indexing="ij")
+    ph = np.arange(B, dtype=np.float32).reshape(B, 1, 1) * 0.7
+    u = np.sin(2 * np.pi * 2 * xx / W + ph) + np.cos(2 * np.pi * 3 * yy / H - ph)
+    v = np.cos(2 * np.pi * 2 * xx / W - ph) - np.sin(2 * np.pi * 3 * yy / H + ph)
+    smooth = np.stack([u, v], 1).astype(np.float32)
+    pile = smooth.copy()
+    pile[:, 0] += W / 8.0
+    contract = np.stack([0.9 * ((W - 1) / 2.0 - xx), 0.9 * ((H - 1) / 2.0 - yy)])[None].repeat(B, 0)
+    return {"smooth": smooth, "pile": pile, "contract": contract.astype(np.float32)}
+
+
+@pytest.mark.parametrize("form", ["production", "persist"])
+@pytest.mark.parametrize("pad", ["border", "zeros"])
+@pytest.mark.parametrize("shape", [(16, 128, 8, 26), (16, 96, 16, 52), (16, 64, 32, 104), (16, 32, 64, 208)])
+def test_warp_persist_production_shapes_vs_oracle(hip_device, shape, pad, form, monkeypatch):
+    """the warp backward at the decoder's four warp sites at
+    batch 16 against the CPU oracle (oracle/warp.py, restating
+    utils/warp_utils.py:97-106 + ATen's sampler), as a call SEQUENCE on one
+    workspace: smooth, border-piling, contracting, smooth again. ``persist``
+    forces the persistent two-launch form (usf_warp_bwd_persist_f32, whose
+    workspace carries a parity word, dirty-tile marks and an overflow buffer
+    from call to call) at every level; ``production`` is ops.warp_backward's
+    own choice per level (ops.WARP_PERSIST_MAX_PIXELS). Tolerances of SURVEY
+    8(c): grad_x and grad_flow atol 1e-4, rtol 1e-5."""
+    import numpy as np
+
+    from oracle import hashrng
+    from oracle.warp import warp_backward_np
+
+    if form == "persist":
+        monkeypatch.setattr(ops, "WARP_PERSIST_MAX_PIXELS", None)
+    B, C, H, W = shape
+    x = hashrng.uniform(shape, 900 + C)
+    g = hashrng.normal(shape, 901 + C)
+    tx, tg = torch.from_numpy(x).to(hip_device), torch.from_numpy(g).to(hip_device)
+    fields = _np_fields(B, H, W)
+    ops.clear_persistent_workspaces()
+    for kind in ("smooth", "pile", "contract", "smooth"):
+        flow = fields[kind]
+        gx, gf = ops.warp_backward(tx, torch.from_numpy(flow).to(hip_device), tg, pad, True, True)
+        rx, rf = warp_backward_np(x, flow, g, pad)
+        np.testing.assert_allclose(gx.cpu().numpy(), rx, atol=1e-4, rtol=1e-5, err_msg=f"{shape} {pad} {kind} gx")
+        np.testing.assert_allclose(gf.cpu().numpy(), rf, atol=1e-4, rtol=1e-5, err_msg=f"{shape} {pad} {kind} gflow")
+    persisted = (hip_device.index, "warp_bwd", shape) in ops._PERSIST
+    assert persisted == (form == "persist" or ops.WARP_PERSIST_MAX_PIXELS is None or H * W <= ops.WARP_PERSIST_MAX_PIXELS)
+
+
+def test_persistent_workspace_cache_is_bounded_and_ordered(hip_device, monkeypatch):
+    """the cache keeps at most PERSIST_MAX_ENTRIES shapes (least
+    recently used out), and a use from another stream is ordered after the
+    previous one (the new stream waits for the owning stream)."""
+    monkeypatch.setattr(ops, "WARP_PERSIST_MAX_PIXELS", None)
+    ops.clear_persistent_workspaces()
+    for i in range(ops.PERSIST_MAX_ENTRIES + 5):
+        ops.persistent_workspace(hip_device, "test_op", (i,), 64)
+    keys = [k for k in ops._PERSIST if k[1] == "test_op"]
+    assert len(keys) == ops.PERSIST_MAX_ENTRIES and keys[0][2] == (5,)
+    # a warp call on a side stream right after one on the main stream gives the same result
+    B, C, H, W = 2, 16, 40, 64
+    gen = torch.Generator(device=hip_device).manual_seed(5)
+    x = torch.randn(B, C, H, W, device=hip_device, generator=gen)
+    go = torch.randn(B, C, H, W, device=hip_device, generator=gen)
+    f = _fields(B, H, W, hip_device)
+    ref = ops.warp_backward(x, f["contract"], go, "border")
+    side = torch.cuda.Stream(hip_device)
+    side.wait_stream(torch.cuda.current_stream(hip_device))
+    with torch.cuda.stream(side):
+        a = ops.warp_backward(x, f["contract"], go, "border")
+        assert ops._PERSIST[(hip_device.index, "warp_bwd", (B, C, H, W))][1] == side
+    b = ops.warp_backward(x, f["contract"], go, "border")  # main stream again: waits for the side stream
+    torch.cuda.synchronize()
+    for r, s1, s2 in zip(ref, a, b):
+        torch.testing.assert_close(s1, r, atol=1e-5, rtol=1e-5)
+        torch.testing.assert_close(s2, r, atol=1e-5, rtol=1e-5)
+    ops.clear_persistent_workspaces()

@@ -1356,25 +1356,16 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(USF_BWD
   // they cut the FETCH traffic (2.6x -> 1.4x of algorithmic). Short chunks
   // (below) keep both.
   int w = linear_block();
-#ifndef USF_BWD_DIRFAST
-#define USF_BWD_DIRFAST 0
-#endif
 #ifndef USF_BWD_GROUP_XCD
 #define USF_BWD_GROUP_XCD 1
 #endif
 #ifndef USF_BWD_SAMPLE_RING
 #define USF_BWD_SAMPLE_RING 1
 #endif
-#ifndef USF_BWD_DIRFAST_CHUNK
-#define USF_BWD_DIRFAST_CHUNK 28
-#endif
-  // direction fastest (MODE 3, chunked levels): a tile's gx1 and gx2 items are
-  // neighbours in one XCD chunk (same L2, same time), so the second read of
-  // its g slice hits L2. Measured at L4, batch 16 (profiles/ab_r02/bwd_dirfast_pmc.json):
-  // FETCH 215.6 -> 157.9 MB per launch (traffic 1.48x -> 1.16x of algorithmic)
-  // at the same replayed time (69.9 vs 67.8 us), but 6 us slower inside the
-  // training step (rocprof: 75.7 vs 69.6 us, profiles/r02_v3_*): off by default.
-  const bool dirfast = MODE == 3 && USF_BWD_DIRFAST && USF_BWD_CHUNK > 0 && gridDim.x >= 16;
+  // (A direction-fastest order -- a tile's gx1 and gx2 items neighbours in one
+  // XCD chunk, so the second read of its g slice hits L2 -- cut FETCH 215.6 ->
+  // 157.9 MB per L4 launch at the same replayed time but ran 6 us slower in the
+  // step, profiles/ab_r02/bwd_dirfast_pmc.json and r02_v3_*; removed in round 6.)
   const int nitems = gridDim.x * gridDim.y * gridDim.z;
   const int per_sample = gridDim.x * gridDim.y;  // work items of one (sample, direction)
   if (NB > 2 && USF_BWD_SAMPLE_RING && nitems >= 8 * per_sample) {
@@ -1390,7 +1381,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(USF_BWD
     // gets a mix of samples and directions. L4 59.5 -> 54.5 us, L3 43 -> 40 us
     // (profiles/ab_r01/bwd_chunk_*.json); whole-sample chunks (xcd_remap) are
     // slower (84 us) and so are levels with < 16 tiles (L1 11.6 -> 13.5 us).
-    w = xcd_chunk(w, gridDim.x * gridDim.y * gridDim.z, dirfast ? USF_BWD_DIRFAST_CHUNK : USF_BWD_CHUNK);
+    w = xcd_chunk(w, gridDim.x * gridDim.y * gridDim.z, USF_BWD_CHUNK);
   } else if (USF_BWD_GROUP_XCD && gridDim.y > 1) {
     // Otherwise small grids that split a tile's channels over gridDim.y groups
     // (each loads the tile's whole g slice): one XCD chunk per tile's groups. In
@@ -1399,17 +1390,9 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(USF_BWD
     // profiles/ab_r05/corr_bwd_group_xcd.json).
     w = xcd_chunk(w, nitems, gridDim.y);
   }
-  int group, tile, b;
-  if (dirfast) {
-    const int dir = w & 1, w2 = w >> 1;
-    group = w2 % gridDim.y;
-    tile = (w2 / gridDim.y) % gridDim.x;
-    b = w2 / (gridDim.x * gridDim.y) + (dir ? B : 0);
-  } else {
-    group = w % gridDim.y;
-    tile = (w / gridDim.y) % gridDim.x;
-    b = w / (gridDim.x * gridDim.y);
-  }
+  const int group = w % gridDim.y;
+  const int tile = (w / gridDim.y) % gridDim.x;
+  const int b = w / (gridDim.x * gridDim.y);
   if constexpr (MODE == 1) {
     corr_bwd_tile<D, PX, SEGX, NW, CC, V, false, AM, NB>(sm, x2, g, gx1, tile, group, b, C, H, W, tiles_x, cg, ep);
   } else if constexpr (MODE == 2) {
@@ -1481,18 +1464,19 @@ hipError_t launch_bwd(const float* x1, const float* x2, const float* g, float* g
   return launch_bwd_v<D, PX, SEGX, NW, CC, 1, NB>(x1, x2, g, gx1, gx2, B, C, H, W, s, ep);
 }
 
+// Tuning hook: usf_set_variant(1, i) forces candidate i for d=4: 0 = the
+// two-image tile (the tile-rich levels' default), 1 = the four-image ring (the
+// small grids' default). (CC = 8 and nine-wave forms were measured slower in
+// rounds 1-4 -- profiles/ab_r01/bwd_variants_b16.txt -- and removed in round 6.)
 hipError_t bwd_candidate_d4(int i, const float* x1, const float* x2, const float* g, float* gx1,
                             float* gx2, int B, int C, int H, int W, hipStream_t s, BwdEpi ep) {
   switch (i) {
     case 0: return launch_bwd<4, 4, 8, 3, 4>(x1, x2, g, gx1, gx2, B, C, H, W, s, ep);
-    case 1: return launch_bwd<4, 4, 8, 3, 8>(x1, x2, g, gx1, gx2, B, C, H, W, s, ep);
-    case 2: return launch_bwd<4, 4, 8, 9, 4>(x1, x2, g, gx1, gx2, B, C, H, W, s, ep);
-    case 3: return launch_bwd<4, 4, 8, 9, 8>(x1, x2, g, gx1, gx2, B, C, H, W, s, ep);
-    case 4: return launch_bwd<4, 4, 8, 3, 4, 4>(x1, x2, g, gx1, gx2, B, C, H, W, s, ep);
+    case 1: return launch_bwd<4, 4, 8, 3, 4, 4>(x1, x2, g, gx1, gx2, B, C, H, W, s, ep);
     default: return hipErrorInvalidValue;
   }
 }
-constexpr int kBwdCandidates = 5;
+constexpr int kBwdCandidates = 2;
 
 // Small grids take the 4-image ring: at most this many (tile, direction, sample)
 // units. There every workgroup's channel loop is short (2-6 stages), and with
@@ -1561,7 +1545,7 @@ namespace {
 
 static int g_variant[4] = {-1, -1, -1, -1};
 int variant_override(int op) { return __atomic_load_n(&g_variant[op], __ATOMIC_RELAXED); }
-int variant_count(int op) { return op == 0 ? kFwdCandidates : op == 1 ? kBwdCandidates : op == 2 ? 8 : 1; }
+int variant_count(int op) { return op == 0 ? kFwdCandidates : op == 1 ? kBwdCandidates : op == 2 ? 3 : 1; }
 void set_variant_override(int op, int index) { __atomic_store_n(&g_variant[op], index, __ATOMIC_RELAXED); }
 
 hipError_t corr_fwd_launch(const float* x1, const float* x2, float* out, int B, int C, int H,

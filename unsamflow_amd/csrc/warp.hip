@@ -309,14 +309,6 @@ __global__ __launch_bounds__(256) void warp_bwd_pair_kernel(const float* __restr
   }
 }
 
-// grad_x gather (warp_gx_gather_kernel) covers source pixels whose flow is
-// below kGatherR pixels in both components ("inliers"); the scatter below,
-// with OUTL, adds the rest.
-constexpr int kGatherR = 2;
-__device__ __forceinline__ bool gather_inlier(float u, float v) {
-  return fabsf(u) < (float)kGatherR && fabsf(v) < (float)kGatherR;  // false for NaN
-}
-
 // grad_x by a binned gather (the default with a caller workspace,
 // usf_warp_bwd_ex_f32). Each source pixel p is filed, by the first pass, under
 // its north-west corner cell nw(p) (a cell grid extended by one row and column
@@ -363,7 +355,7 @@ struct BinArgs {
   int tiles_x = 0, ntiles = 0; // the gather's 32 x 8 target tiles
 };
 
-template <bool BORDER, bool WANT_GX, bool WANT_GF, int CS, int OUTL = 0, int BIN = 0>
+template <bool BORDER, bool WANT_GX, bool WANT_GF, int CS, int BIN = 0>
 __global__ __launch_bounds__(256) void warp_bwd_kernel(const float* __restrict__ x,
                                                        const float* __restrict__ flow,
                                                        long long fbs,
@@ -390,11 +382,9 @@ __global__ __launch_bounds__(256) void warp_bwd_kernel(const float* __restrict__
     const int y = p / W, xx = p - y * W;
     const float* fb = flow + b * fbs;
     const float u = fb[p], v = fb[HW + p];
-    if (OUTL == 1) valid = !gather_inlier(u, v);  // the gather kernel has the inliers
     tp = make_tap(u, v, xx, y, H, W, BORDER);
   }
   if (!valid) tp.m_nw = tp.m_ne = tp.m_sw = tp.m_se = false;
-  if (OUTL && !__syncthreads_or(valid)) return;  // no outlier in this workgroup (uniform)
   bool ovf = false;  // BIN == 2: p did not get a slot; its contributions go to ba.ovfgx
   if (BIN && slice == 0 && valid) {
     // file p under its north-west corner cell (see BinArgs); weights as the scatter forms them
@@ -827,266 +817,6 @@ __global__ __launch_bounds__(256) void warp_gx_ovf_kernel(const float* __restric
   }
 }
 
-// grad_x as a gather (no atomics for inliers, no zero fill; usf_set_variant(2, 4)). A workgroup
-// owns a GTW x GTH tile of target cells and GCC channels. Phase 1: the taps of
-// every source pixel within kGatherR + 1 of the tile (make_tap, the same
-// coordinate chain as the scatter) go to LDS -- the north-west corner packed
-// relative to the tile and the four corner weights, zeroed where a corner is
-// off-image; sources that are not inliers get no corner. Phase 2: each thread
-// (one target cell q) scans the (2R+3)^2 sources that can reach q, in a fixed
-// order; a source whose corner is q adds weight * gout[c][source] for the
-// workgroup's channels. Sources with |flow| >= R are added afterwards by the
-// scatter (warp_bwd_kernel<..., OUTL>).
-constexpr int GTW = 32, GTH = 8, GCC = 16;
-constexpr int GWX = GTW + 2 * kGatherR + 2, GWY = GTH + 2 * kGatherR + 2;  // source window
-constexpr int GWN = GWX * GWY;
-constexpr int kGList = 8;  // contributors a cell keeps in its list (more: per-chunk rescan)
-
-template <bool BORDER>
-__global__ __launch_bounds__(256) void warp_gx_gather_kernel(const float* __restrict__ flow, long long fbs,
-                                                             const float* __restrict__ gout,
-                                                             float* __restrict__ gx, int C, int H, int W,
-                                                             int tiles_x, int cgroups, int cper) {
-  constexpr int R = kGatherR;
-  __shared__ int spos[GWN];        // (yn - wy0) << 16 | (xw - wx0), or -1: no corner
-  __shared__ float swt[4][GWN];    // nw, ne, sw, se weights (0 where masked)
-  __shared__ int lsrc[kGList][256];  // per-cell contributor lists (source offset, weight)
-  __shared__ float lwt[kGList][256];
-  const int HW = H * W;
-  const int t = threadIdx.x;
-  const int tile = blockIdx.x;
-  const int b = blockIdx.y / cgroups, cgrp = blockIdx.y - b * cgroups;
-  const int ty = tile / tiles_x, tx = tile - ty * tiles_x;
-  const int x0 = tx * GTW, y0 = ty * GTH;
-  const int wx0 = x0 - R - 1, wy0 = y0 - R - 1;  // window origin (source coordinates)
-  const float* fb = flow + b * fbs;
-  for (int i = t; i < GWN; i += 256) {
-    const int sy = wy0 + i / GWX, sx = wx0 + i % GWX;
-    int pos = -1;
-    float w4[4] = {0.f, 0.f, 0.f, 0.f};
-    if ((unsigned)sy < (unsigned)H && (unsigned)sx < (unsigned)W) {
-      const int s = sy * W + sx;
-      const float u = fb[s], v = fb[HW + s];
-      if (gather_inlier(u, v)) {
-        const Tap tp = make_tap(u, v, sx, sy, H, W, BORDER);
-        // inliers land within R + 1 of the source; a corner left of / above the
-        // window makes pos negative (it reaches no cell of the tile)
-        pos = ((tp.yn - wy0) << 16) | (tp.xw - wx0);
-        w4[0] = tp.m_nw ? tp.s * tp.e : 0.f;
-        w4[1] = tp.m_ne ? tp.s * tp.w : 0.f;
-        w4[2] = tp.m_sw ? tp.n * tp.e : 0.f;
-        w4[3] = tp.m_se ? tp.n * tp.w : 0.f;
-      }
-    }
-    spos[i] = pos;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) swt[k][i] = w4[k];
-  }
-  __syncthreads();
-  const int qx = x0 + (t % GTW), qy = y0 + (t / GTW);
-  if (qx >= W || qy >= H) return;  // no barrier below
-  const int rx = qx - wx0, ry = qy - wy0;  // q relative to the window
-  // the sources within R + 1 of q whose corner is q, in a fixed scan order
-  auto scan = [&](auto&& take) {
-    for (int dy = -R - 1; dy <= R + 1; ++dy) {
-      for (int dx = -R - 1; dx <= R + 1; ++dx) {
-        const int i = (ry + dy) * GWX + (rx + dx);
-        const int pos = spos[i];
-        if (pos < 0) continue;
-        const int cx = rx - (pos & 0xFFFF), cy = ry - (pos >> 16);  // q - north-west corner
-        if ((unsigned)cx > 1u || (unsigned)cy > 1u) continue;
-        const float w = swt[cy * 2 + cx][i];
-        if (w == 0.f) continue;
-        take((wy0 + ry + dy) * W + (wx0 + rx + dx), w);
-      }
-    }
-  };
-  int cnt = 0;
-  scan([&](int s, float w) {
-    if (cnt < kGList) {
-      lsrc[cnt][t] = s;
-      lwt[cnt][t] = w;
-    }
-    ++cnt;
-  });
-  const int cbeg = cgrp * cper, cend = min(C, cbeg + cper);
-  const float* gb = gout + (size_t)b * C * HW;
-  float* gq = gx + (size_t)b * C * HW + qy * W + qx;
-  const bool overflow = __any(cnt > kGList);  // converging flow: rescan per channel chunk
-  for (int c0 = cbeg; c0 < cend; c0 += GCC) {
-    float acc[GCC];
-#pragma unroll
-    for (int c = 0; c < GCC; ++c) acc[c] = 0.f;
-    auto add = [&](int s, float w) {
-#pragma unroll
-      for (int c = 0; c < GCC; ++c)
-        if (c0 + c < cend) acc[c] = fmaf(w, gb[(size_t)(c0 + c) * HW + s], acc[c]);
-    };
-    if (overflow) {
-      scan(add);
-    } else {
-      // list slot j of every lane at once: no divergence between the lanes'
-      // different source positions (same order as the scan)
-      for (int j = 0; j < kGList; ++j) {
-        if (!__any(j < cnt)) break;
-        const bool has = j < cnt;
-        add(has ? lsrc[j][t] : qy * W + qx, has ? lwt[j][t] : 0.f);
-      }
-    }
-#pragma unroll
-    for (int c = 0; c < GCC; ++c)
-      if (c0 + c < cend) gq[(size_t)(c0 + c) * HW] = acc[c];
-  }
-}
-
-// grad_x with the corner scatter pre-summed in LDS. A workgroup owns a 2-D
-// tile of TW x TH source pixels (TW*TH = 256/CS) x CS channel slices. With a
-// smooth flow the tile's 4*TW*TH*C corner targets fall in a small box; the
-// box is found by an LDS min/max reduction, zeroed in LDS, filled with
-// ds_add_f32 (LDS float atomics) and then flushed with ONE global atomic per
-// touched cell, row-contiguous across lanes: ~3-4x fewer global atomics than
-// one per corner. A tile whose box exceeds kAggCap floats (large or
-// discontinuous flow) falls back to direct global atomics. grad_flow (if
-// requested) is computed in the same channel loop and combined over the
-// slices in a fixed order, as in warp_bwd_kernel.
-constexpr int kAggCap = 8192;
-
-template <bool BORDER, bool WANT_GF, int CS, bool LDS_AGG>
-__global__ __launch_bounds__(256) void warp_bwd_gx_kernel(const float* __restrict__ x,
-                                                          const float* __restrict__ flow,
-                                                          long long fbs,
-                                                          const float* __restrict__ gout,
-                                                          float* __restrict__ gx,
-                                                          float* __restrict__ gflow, int B, int C,
-                                                          int H, int W, int tiles_x) {
-  constexpr int TPX = 256 / CS;
-  constexpr int TW = TPX >= 16 ? 16 : TPX;
-  constexpr int TH = TPX / TW;
-  __shared__ float agg[kAggCap];
-  __shared__ float red[2][256];
-  __shared__ int box[4];  // x lo, x hi, y lo, y hi of in-image corner targets
-  const int HW = H * W;
-  const int t = threadIdx.x;
-  const int slice = t / TPX;
-  const int pl = t - slice * TPX;
-  const int b = blockIdx.y;
-  const int ty = blockIdx.x / tiles_x;
-  const int tx = blockIdx.x - ty * tiles_x;
-  const int py = ty * TH + pl / TW, pxx = tx * TW + pl % TW;
-  const bool valid = py < H && pxx < W;
-  const int p = py * W + pxx;
-  Tap tp{};
-  if (valid) {
-    const float* fb = flow + b * fbs;
-    tp = make_tap(fb[p], fb[HW + p], pxx, py, H, W, BORDER);
-  }
-  if (t == 0) {
-    box[0] = INT_MAX; box[1] = INT_MIN; box[2] = INT_MAX; box[3] = INT_MIN;
-  }
-  __syncthreads();
-  {
-    // wave-level min/max with shuffles, then one LDS atomic per wave (a
-    // same-address LDS atomic from every lane serialises 64-fold)
-    const bool hit = valid && slice == 0 && (tp.m_nw || tp.m_ne || tp.m_sw || tp.m_se);
-    int xl = hit ? max(tp.xw, 0) : INT_MAX, xh = hit ? min(tp.xw + 1, W - 1) : INT_MIN;
-    int yl = hit ? max(tp.yn, 0) : INT_MAX, yh = hit ? min(tp.yn + 1, H - 1) : INT_MIN;
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-      xl = min(xl, __shfl_xor(xl, off));
-      xh = max(xh, __shfl_xor(xh, off));
-      yl = min(yl, __shfl_xor(yl, off));
-      yh = max(yh, __shfl_xor(yh, off));
-    }
-    if ((t & 63) == 0 && xh >= xl) {
-      atomicMin(&box[0], xl);
-      atomicMax(&box[1], xh);
-      atomicMin(&box[2], yl);
-      atomicMax(&box[3], yh);
-    }
-  }
-  __syncthreads();
-  const int bx0 = box[0], by0 = box[2];
-  const int bw = box[1] - bx0 + 1, bh = box[3] - by0 + 1;
-  const bool any = box[1] >= box[0];
-  const bool use_lds = LDS_AGG && any && (long)bw * bh * C <= kAggCap;  // block-uniform
-  const int area = use_lds ? bw * bh : 0;
-  if (use_lds) {
-    for (int i = t; i < C * area; i += 256) agg[i] = 0.f;
-    __syncthreads();
-  }
-
-  float dix = 0.f, diy = 0.f;
-  if (valid) {
-    const float wnw = tp.s * tp.e, wne = tp.s * tp.w, wsw = tp.n * tp.e, wse = tp.n * tp.w;
-    const float* xb = x + (size_t)b * C * HW;
-    const float* gb = gout + (size_t)b * C * HW + p;
-    float* gxb = gx + (size_t)b * C * HW;
-    // LDS offsets of the 4 corners inside the box (valid only when masked in)
-    const int lx = tp.xw - bx0, ly = tp.yn - by0;
-    const int a_nw = ly * bw + lx, a_ne = a_nw + 1, a_sw = a_nw + bw, a_se = a_sw + 1;
-#pragma unroll 4
-    for (int c = slice; c < C; c += CS) {
-      const float go = gb[(size_t)c * HW];
-      if (use_lds) {
-        float* ac = agg + c * area;
-        if (tp.m_nw) atomicAdd(ac + a_nw, go * wnw);
-        if (tp.m_ne) atomicAdd(ac + a_ne, go * wne);
-        if (tp.m_sw) atomicAdd(ac + a_sw, go * wsw);
-        if (tp.m_se) atomicAdd(ac + a_se, go * wse);
-      } else {
-        float* gc = gxb + (size_t)c * HW;
-        if (tp.m_nw) atomicAdd(gc + tp.o_nw, go * wnw);
-        if (tp.m_ne) atomicAdd(gc + tp.o_ne, go * wne);
-        if (tp.m_sw) atomicAdd(gc + tp.o_sw, go * wsw);
-        if (tp.m_se) atomicAdd(gc + tp.o_se, go * wse);
-      }
-      if (WANT_GF) {
-        const float* xc = xb + (size_t)c * HW;
-        const float vnw = tp.m_nw ? xc[tp.o_nw] : 0.f;
-        const float vne = tp.m_ne ? xc[tp.o_ne] : 0.f;
-        const float vsw = tp.m_sw ? xc[tp.o_sw] : 0.f;
-        const float vse = tp.m_se ? xc[tp.o_se] : 0.f;
-        dix += ((vne - vnw) * tp.s + (vse - vsw) * tp.n) * go;
-        diy += ((vsw - vnw) * tp.e + (vse - vne) * tp.w) * go;
-      }
-    }
-  }
-  if (use_lds) {
-    __syncthreads();
-    // flush row by row: lanes run along the box row (contiguous global
-    // addresses); one global atomic per touched cell
-    float* gxb = gx + (size_t)b * C * HW + by0 * W + bx0;
-    const int nrows = C * bh;
-    for (int row = t / 64; row < nrows; row += 4) {
-      const int c = row / bh, iy = row - (row / bh) * bh;
-      const float* src = agg + row * bw;
-      float* dst = gxb + (size_t)c * HW + iy * W;
-      for (int ix = t & 63; ix < bw; ix += 64) {
-        const float v = src[ix];
-        if (v != 0.f) atomicAdd(dst + ix, v);
-      }
-    }
-  }
-  if (WANT_GF) {
-    if (CS > 1) {
-      red[0][t] = dix;
-      red[1][t] = diy;
-      __syncthreads();
-      if (slice != 0) return;
-#pragma unroll
-      for (int k = 1; k < CS; ++k) {
-        dix += red[0][pl + k * TPX];
-        diy += red[1][pl + k * TPX];
-      }
-    }
-    if (!valid) return;
-    const float ggx = dix * tp.mx, ggy = diy * tp.my;
-    float* gf = gflow + (size_t)b * 2 * HW + p;
-    gf[0] = (ggx / (float)(W - 1)) * 2.0f;
-    gf[HW] = (ggy / (float)(H - 1)) * 2.0f;
-  }
-}
-
 // Channel slices per workgroup: the smallest CS in {1,4,16,64} giving >= 1024
 // workgroups (8 XCDs x 32 CUs x 4), capped by C.
 inline int pick_cs(int B, int C, int HW) {
@@ -1122,37 +852,15 @@ template <bool BORDER, int CS>
 void bwd_launch_cs(const float* x, const float* flow, long long fbs, const float* gout, float* gx,
                    float* gflow, int B, int C, int H, int W, hipStream_t s) {
   const dim3 grid((unsigned)((H * W + 256 / CS - 1) / (256 / CS)), (unsigned)B), block(256);
-  if (gx) {
-    constexpr int TPX = 256 / CS, TW = TPX >= 16 ? 16 : TPX, TH = TPX / TW;
-    const int tiles_x = (W + TW - 1) / TW, tiles_y = (H + TH - 1) / TH;
-    const dim3 g2((unsigned)(tiles_x * tiles_y), (unsigned)B);
-    // usf_set_variant(2, v): 1 = LDS-aggregated tiles; otherwise lane-merged direct atomics
-    const int v = variant_override(2);
-    if (v != 1) {
-      if (gflow)
-        hipLaunchKernelGGL((warp_bwd_kernel<BORDER, true, true, CS>), grid, block, 0, s, x, flow,
-                           fbs, gout, gx, gflow, B, C, H, W);
-      else
-        hipLaunchKernelGGL((warp_bwd_kernel<BORDER, true, false, CS>), grid, block, 0, s, x, flow,
-                           fbs, gout, gx, gflow, B, C, H, W);
-      return;
-    }
-    const bool agg = true;
-    if (gflow && agg)
-      hipLaunchKernelGGL((warp_bwd_gx_kernel<BORDER, true, CS, true>), g2, block, 0, s, x, flow,
-                         fbs, gout, gx, gflow, B, C, H, W, tiles_x);
-    else if (gflow)
-      hipLaunchKernelGGL((warp_bwd_gx_kernel<BORDER, true, CS, false>), g2, block, 0, s, x, flow,
-                         fbs, gout, gx, gflow, B, C, H, W, tiles_x);
-    else if (agg)
-      hipLaunchKernelGGL((warp_bwd_gx_kernel<BORDER, false, CS, true>), g2, block, 0, s, x, flow,
-                         fbs, gout, gx, gflow, B, C, H, W, tiles_x);
-    else
-      hipLaunchKernelGGL((warp_bwd_gx_kernel<BORDER, false, CS, false>), g2, block, 0, s, x, flow,
-                         fbs, gout, gx, gflow, B, C, H, W, tiles_x);
-  } else
-    hipLaunchKernelGGL((warp_bwd_kernel<BORDER, false, true, CS>), grid, block, 0, s, x, flow,
-                       fbs, gout, gx, gflow, B, C, H, W);
+  if (gx && gflow)
+    hipLaunchKernelGGL((warp_bwd_kernel<BORDER, true, true, CS>), grid, block, 0, s, x, flow, fbs, gout, gx, gflow,
+                       B, C, H, W);
+  else if (gx)
+    hipLaunchKernelGGL((warp_bwd_kernel<BORDER, true, false, CS>), grid, block, 0, s, x, flow, fbs, gout, gx, gflow,
+                       B, C, H, W);
+  else
+    hipLaunchKernelGGL((warp_bwd_kernel<BORDER, false, true, CS>), grid, block, 0, s, x, flow, fbs, gout, gx, gflow,
+                       B, C, H, W);
 }
 
 template <bool BORDER, int CS>
@@ -1166,28 +874,6 @@ void bwd_pair_cs(const float* x, const float* flow, long long fbs, const float* 
   else
     hipLaunchKernelGGL((warp_bwd_pair_kernel<BORDER, false, CS>), grid, block, 0, s, x, flow, fbs, gout, gx,
                        gflow, B, C, H, W);
-}
-
-// grad_x by gather (+ the scatter for |flow| >= kGatherR), grad_flow by the
-// scatter kernel's channel reduction without its grad_x part.
-template <bool BORDER, int CS>
-void bwd_gather_cs(const float* x, const float* flow, long long fbs, const float* gout, float* gx,
-                   float* gflow, int B, int C, int H, int W, hipStream_t s) {
-  const dim3 grid((unsigned)((H * W + 256 / CS - 1) / (256 / CS)), (unsigned)B), block(256);
-  if (gflow)
-    hipLaunchKernelGGL((warp_bwd_kernel<BORDER, false, true, CS>), grid, block, 0, s, x, flow, fbs, gout,
-                       nullptr, gflow, B, C, H, W);
-  const int tiles_x = (W + GTW - 1) / GTW, tiles_y = (H + GTH - 1) / GTH;
-  // channel groups only where the tiles alone give few workgroups (L1: 16)
-  const int chunks = (C + GCC - 1) / GCC;
-  const long units = (long)tiles_x * tiles_y * B;
-  const int want = (int)std::min<long>(chunks, std::max<long>(1, (512 + units - 1) / units));
-  const int cper = ((chunks + want - 1) / want) * GCC;
-  const int cgroups = (C + cper - 1) / cper;
-  hipLaunchKernelGGL((warp_gx_gather_kernel<BORDER>), dim3((unsigned)(tiles_x * tiles_y), (unsigned)(B * cgroups)),
-                     block, 0, s, flow, fbs, gout, gx, C, H, W, tiles_x, cgroups, cper);
-  hipLaunchKernelGGL((warp_bwd_kernel<BORDER, true, false, CS, 1>), grid, block, 0, s, x, flow, fbs, gout,
-                     gx, nullptr, B, C, H, W);
 }
 
 // Binned-gather workspace: overflow count and cell counts (zeroed per call),
@@ -1247,10 +933,10 @@ void bin_pass_cs(const float* x, const float* flow, long long fbs, const float* 
                  int C, int H, int W, BinArgs ba, hipStream_t s) {
   const dim3 grid((unsigned)((H * W + 256 / CS - 1) / (256 / CS)), (unsigned)B), block(256);
   if (gflow)
-    hipLaunchKernelGGL((warp_bwd_kernel<BORDER, false, true, CS, 0, BINM>), grid, block, 0, s, x, flow, fbs,
+    hipLaunchKernelGGL((warp_bwd_kernel<BORDER, false, true, CS, BINM>), grid, block, 0, s, x, flow, fbs,
                        gout, nullptr, gflow, B, C, H, W, ba);
   else
-    hipLaunchKernelGGL((warp_bwd_kernel<BORDER, false, false, CS, 0, BINM>), grid, block, 0, s, x, flow,
+    hipLaunchKernelGGL((warp_bwd_kernel<BORDER, false, false, CS, BINM>), grid, block, 0, s, x, flow,
                        fbs, gout, nullptr, nullptr, B, C, H, W, ba);
 }
 
@@ -1377,294 +1063,44 @@ void bwd_bins_persist(const float* x, const float* flow, long long fbs, const fl
                      0, s, gout, ba, gx, C, H, W, gg.tiles_x, gg.cper);
 }
 
-// --------------------------------------------------- small-image backward --
-// Decoder level 1 (batch 16 x 128 x 8 x 26: 208 pixels a sample): the binned
-// gather is four launches of a few workgroups each, ~20 us of latency chains.
-// Here ONE launch of two kinds of 1024-thread workgroups does both gradients,
-// deterministically, each workgroup in one load round trip:
-//  * grad_x, one workgroup per (sample, group of kSmallCG channels): it stages
-//    the group's grad_out planes in LDS and computes every pixel's tap (the
-//    reference chain, make_tap). Thread q (< HW) then lists the (pixel, corner)
-//    pairs that land on cell q by scanning the taps in pixel order -- a fixed
-//    summation order with no atomics and no sort -- keeping the first kSmallM
-//    in registers and the rest of a crowded cell in an LDS pool; thread
-//    (cell, slice) sums weight * grad_out over the list for its channels;
-//  * grad_flow, one workgroup per (sample, 64 pixels): thread (pixel, slice)
-//    accumulates its channels' tap derivative terms from direct loads (all in
-//    flight at once), and the 16 slices are added in a fixed order.
-// Opt-in (usf_set_variant(2, 7)): measured slower than the binned gather
-// (profiles/ab_r03/warp_small.json); -DUSF_WARP_SMALL=1 makes it the default
-// where it fits.
-#ifndef USF_WARP_SMALL
-#define USF_WARP_SMALL 0
-#endif
-constexpr int kSmallNT = 1024;
-constexpr int kSmallMaxHW = 256;
-#ifndef USF_WARP_SMALL_CG
-#define USF_WARP_SMALL_CG 32
-#endif
-constexpr int kSmallCG = USF_WARP_SMALL_CG;  // channels per grad_x workgroup
-static_assert(kSmallCG % (kSmallNT / kSmallMaxHW) == 0, "whole channels per (cell, slice) thread");
-constexpr int kSmallM = 8;     // list entries a thread keeps in registers
-constexpr int kSmallPool = 4 * kSmallMaxHW;
-constexpr int kSmallLD = (kSmallCG * kSmallMaxHW + kSmallNT - 1) / kSmallNT;  // staged floats per thread
-constexpr int kSmallGFP = 64;  // pixels per grad_flow workgroup (x 16 channel slices)
-// Static LDS of warp_bwd_small_kernel (below): about 64 KiB at kSmallCG = 32,
-// which needs gfx950's 160 KiB per workgroup (64 KiB targets cannot build it).
-constexpr int kSmallLdsBytes = kSmallMaxHW * (16 + 16 + 4 + 4 + kSmallM * (2 + 4) + 4 * kSmallCG) +
-                               kSmallPool * 2 + 2 * kSmallNT * 4 + 4 * 5;
-static_assert(kSmallLdsBytes <= 160 * 1024, "warp_bwd_small_kernel: LDS beyond gfx950's 160 KiB per workgroup");
-
-template <bool BORDER>
-__global__ __launch_bounds__(kSmallNT) void warp_bwd_small_kernel(const float* __restrict__ x,
-                                                                  const float* __restrict__ flow,
-                                                                  long long fbs,
-                                                                  const float* __restrict__ gout,
-                                                                  float* __restrict__ gx,
-                                                                  float* __restrict__ gflow, int B, int C,
-                                                                  int H, int W, int ngx) {
-  __shared__ int4 tof[kSmallMaxHW];    // corner target cells (-1: off the image)
-  __shared__ float4 twt[kSmallMaxHW];  // corner weights (nw, ne, sw, se)
-  __shared__ int ltop;                 // pool fill
-  __shared__ int ext[4];               // corner displacement extents: min/max (xw - x), (yn - y)
-  __shared__ int lcnt[kSmallMaxHW], lbeg[kSmallMaxHW];  // a cell's sources; its pool range
-  __shared__ unsigned short lsp[kSmallM][kSmallMaxHW];  // a cell's first kSmallM source pixels
-  __shared__ float lsw[kSmallM][kSmallMaxHW];           // and their weights
-  __shared__ unsigned short pool[kSmallPool];           // pixel * 4 + corner
-  __shared__ float gst[kSmallCG][kSmallMaxHW];          // the group's grad_out planes
-  __shared__ float red[2][kSmallNT];
-  const int HW = H * W;
-  const int t = threadIdx.x;
-  const bool is_gx = (int)blockIdx.x < ngx;
-  const int wi = is_gx ? blockIdx.x : blockIdx.x - ngx;
-  const float* fb0 = flow;
-
-  if (!is_gx) {  // ---- grad_flow of 64 pixels of one sample (uniform branch)
-    constexpr int NSL = kSmallNT / kSmallGFP;  // 16 channel slices
-    const int nblk = (HW + kSmallGFP - 1) / kSmallGFP;
-    const int b = wi / nblk;
-    const int pp = (wi - b * nblk) * kSmallGFP + (t & (kSmallGFP - 1));
-    const int slice = t / kSmallGFP;
-    const bool pin = pp < HW;
-    const int pc = pin ? pp : 0;
-    const float* fb = fb0 + b * fbs;
-    const Tap tp = make_tap(fb[pc], fb[HW + pc], pc % W, pc / W, H, W, BORDER);
-    const float* xb = x + (size_t)b * C * HW;
-    const float* gb = gout + (size_t)b * C * HW;
-    float dix = 0.f, diy = 0.f;
-    // channels slice, slice + 16, ... in batches of 8: 40 loads in flight
-    constexpr int U = 8;
-    for (int cb = slice; cb < C; cb += NSL * U) {
-      float go[U], vnw[U], vne[U], vsw[U], vse[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int c = cb + NSL * u;
-        const bool ok = pin && c < C;
-        const float* xc = xb + (size_t)(ok ? c : 0) * HW;
-        go[u] = ok ? gb[(size_t)c * HW + pc] : 0.f;
-        vnw[u] = ok && tp.m_nw ? xc[tp.o_nw] : 0.f;
-        vne[u] = ok && tp.m_ne ? xc[tp.o_ne] : 0.f;
-        vsw[u] = ok && tp.m_sw ? xc[tp.o_sw] : 0.f;
-        vse[u] = ok && tp.m_se ? xc[tp.o_se] : 0.f;
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        if (cb + NSL * u < C) {
-          dix += ((vne[u] - vnw[u]) * tp.s + (vse[u] - vsw[u]) * tp.n) * go[u];
-          diy += ((vsw[u] - vnw[u]) * tp.e + (vse[u] - vne[u]) * tp.w) * go[u];
-        }
-      }
-    }
-    red[0][t] = dix;
-    red[1][t] = diy;
-    __syncthreads();
-    if (slice != 0 || !pin) return;
-    for (int k = 1; k < NSL; ++k) {  // slices in a fixed order (deterministic)
-      dix += red[0][t + k * kSmallGFP];
-      diy += red[1][t + k * kSmallGFP];
-    }
-    // grid grad, then norm_grid's autograd (DivBackward by (W-1), MulBackward by 2)
-    const float ggx = dix * tp.mx, ggy = diy * tp.my;
-    float* gf = gflow + (size_t)b * 2 * HW + pp;
-    gf[0] = (ggx / (float)(W - 1)) * 2.0f;
-    gf[HW] = (ggy / (float)(H - 1)) * 2.0f;
-    return;
-  }
-
-  // ---- grad_x of channels [c0, c0 + kSmallCG) of sample b
-  constexpr int NS = kSmallNT / kSmallMaxHW;  // channel slices: thread = (cell, slice)
-  const int G = (C + kSmallCG - 1) / kSmallCG;
-  const int b = wi / G;
-  const int c0 = (wi - b * G) * kSmallCG;
-  const int pp = t % HW, slice = t / HW;
-  const float* gb = gout + (size_t)b * C * HW;
-  float v[kSmallLD];  // the group's grad_out planes, issued before the tap chain
-#pragma unroll
-  for (int u = 0; u < kSmallLD; ++u) {
-    const int e = t + kSmallNT * u, c = e / HW, q = e - c * HW;
-    v[u] = c < kSmallCG && c0 + c < C ? gb[(size_t)(c0 + c) * HW + q] : 0.f;
-  }
-  if (t < 4) ext[t] = (t & 1) ? INT_MIN : INT_MAX;
-  if (t == 0) ltop = 0;
-  __syncthreads();
-  if (t < HW) {
-    const float* fb = fb0 + b * fbs;
-    const Tap tp = make_tap(fb[t], fb[HW + t], t % W, t / W, H, W, BORDER);
-    const int4 o = make_int4(tp.m_nw ? tp.o_nw : -1, tp.m_ne ? tp.o_ne : -1, tp.m_sw ? tp.o_sw : -1,
-                             tp.m_se ? tp.o_se : -1);
-    tof[t] = o;
-    twt[t] = make_float4(tp.s * tp.e, tp.s * tp.w, tp.n * tp.e, tp.n * tp.w);
-    if (o.x >= 0 || o.y >= 0 || o.z >= 0 || o.w >= 0) {  // extents of the pixels that land anywhere
-      const int dxw = tp.xw - t % W, dyn = tp.yn - t / W;
-      atomicMin(&ext[0], dxw);
-      atomicMax(&ext[1], dxw);
-      atomicMin(&ext[2], dyn);
-      atomicMax(&ext[3], dyn);
-    }
-  }
-#pragma unroll
-  for (int u = 0; u < kSmallLD; ++u) {
-    const int e = t + kSmallNT * u, c = e / HW, q = e - c * HW;
-    if (c < kSmallCG) gst[c][q] = v[u];
-  }
-  __syncthreads();
-  // thread q < HW lists the sources of cell q: the pixels whose corner cells
-  // can include q (north-west corner within the extents, minus one row /
-  // column), scanned in pixel order; a pixel's 4 corners are 4 different cells,
-  // so at most one matches
-  const bool act = slice < NS;
-  if (t < HW) {
-    const int qy = t / W, qx = t - (t / W) * W;
-    const bool any = ext[0] <= ext[1];  // some pixel lands on the image (else no sources)
-    const int y0 = any ? max(0, qy - 1 - ext[3]) : 1, y1 = any ? min(H - 1, qy - ext[2]) : 0;
-    const int x0 = any ? max(0, qx - 1 - ext[1]) : 1, x1 = any ? min(W - 1, qx - ext[0]) : 0;
-    int n = 0;
-    for (int y = y0; y <= y1; ++y)
-      for (int xx = x0; xx <= x1; ++xx) {
-        const int p = y * W + xx;
-        const int4 o = tof[p];
-        const int k = o.x == t ? 0 : o.y == t ? 1 : o.z == t ? 2 : o.w == t ? 3 : -1;
-        if (k >= 0) {
-          if (n < kSmallM) {
-            const float4 w = twt[p];
-            lsp[n][t] = (unsigned short)p;
-            lsw[n][t] = k == 0 ? w.x : k == 1 ? w.y : k == 2 ? w.z : w.w;
-          }
-          ++n;
-        }
-      }
-    lcnt[t] = n;
-    if (n > kSmallM) {  // crowded cell: the rest of its list in the pool, same order
-      const int beg = atomicAdd(&ltop, n - kSmallM);
-      lbeg[t] = beg;
-      int m = 0;
-      for (int y = y0; y <= y1; ++y)
-        for (int xx = x0; xx <= x1; ++xx) {
-          const int p = y * W + xx;
-          const int4 o = tof[p];
-          const int k = o.x == t ? 0 : o.y == t ? 1 : o.z == t ? 2 : o.w == t ? 3 : -1;
-          if (k >= 0) {
-            if (m >= kSmallM) pool[beg + m - kSmallM] = (unsigned short)(p * 4 + k);
-            ++m;
-          }
-        }
-    }
-  }
-  __syncthreads();
-  if (!act) return;
-  const int n = lcnt[pp];
-  int sp[kSmallM];
-  float sw[kSmallM];
-#pragma unroll
-  for (int j = 0; j < kSmallM; ++j) {
-    sp[j] = j < n ? lsp[j][pp] : 0;
-    sw[j] = j < n ? lsw[j][pp] : 0.f;
-  }
-  const int pb = n > kSmallM ? lbeg[pp] : 0;
-  // entry-major: each source's weight and pixel are read once and its CPT
-  // channels' grad_out reads are independent (a crowded cell's pool entries
-  // no longer form one dependent LDS chain per channel); per channel the
-  // entries still add in list order
-  constexpr int CPT = kSmallCG / NS;
-  float acc[CPT];
-#pragma unroll
-  for (int i = 0; i < CPT; ++i) acc[i] = 0.f;
-  auto add = [&](int p, float w) {
-#pragma unroll
-    for (int i = 0; i < CPT; ++i) acc[i] += gst[slice + NS * i][p] * w;
-  };
-#pragma unroll
-  for (int j = 0; j < kSmallM; ++j)
-    if (j < n) add(sp[j], sw[j]);
-  for (int j = kSmallM; j < n; ++j) {  // crowded cell: the rest of its list from the pool
-    const int e = pool[pb + j - kSmallM], p = e >> 2, k = e & 3;
-    const float4 w = twt[p];
-    add(p, k == 0 ? w.x : k == 1 ? w.y : k == 2 ? w.z : w.w);
-  }
-#pragma unroll
-  for (int i = 0; i < CPT; ++i) {
-    const int c = slice + NS * i;
-    if (c0 + c < C) gx[((size_t)b * C + c0 + c) * HW + pp] = acc[i];
-  }
-}
-
+// grad_x paths (usf_set_variant(2, v), benchmarking only): 0 = the lane-merged
+// scatter (fp32 atomics, one lane per pixel), 1 = the same over vertically
+// adjacent pixel pairs, 2 = the binned gather (needs a workspace); -1 = the
+// built-in choice: with a workspace the binned gather (persistent or per
+// call), without one the pair scatter at large levels and the per-pixel
+// scatter elsewhere. (Round 6 removed the measured-slower paths that no default
+// took: the LDS-aggregated tile scatter, the small-radius gather with its
+// outlier scatter, the small-image one-launch kernel and the forced channel
+// splits -- docs/EXPERIMENTS.md keeps their measurements.)
 template <bool BORDER>
 void bwd_launch_pad(const float* x, const float* flow, long long fbs, const float* gout,
                     float* gx, float* gflow, int B, int C, int H, int W, hipStream_t s,
                     void* ws = nullptr, long long ws_bytes = 0, bool persist = false) {
-  // usf_set_variant(2, 2 / 3): lane-merged scatter with CS forced to 4 / 1
-  // (whole-wave pixel runs) instead of the occupancy-driven choice
   const int v = variant_override(2);
   if (persist) {  // usf_warp_bwd_persist_f32 (capi.cpp checked the workspace size and C)
-    if (gx && (v < 0 || v == 6)) {
+    if (gx && (v < 0 || v == 2)) {
       bwd_bins_persist<BORDER>(x, flow, fbs, gout, gx, gflow, B, C, H, W, ws, s);
       return;
     }
-    // grad_flow only, or a forced variant: the per-call dispatch WITHOUT the
+    // grad_flow only, or a forced scatter: the per-call dispatch WITHOUT the
     // workspace (its layout differs; the persistent state stays untouched)
     ws = nullptr;
     ws_bytes = 0;
   }
-  // small images (decoder level 1): one launch (usf_set_variant(2, 7) where
-  // it fits; off by default, see USF_WARP_SMALL)
-  if ((v == 7 || (v < 0 && USF_WARP_SMALL)) && H * W <= kSmallMaxHW && H >= 2 && W >= 2 && (gx || gflow)) {
-    const int ngx = gx ? B * ((C + kSmallCG - 1) / kSmallCG) : 0;
-    const int ngf = gflow ? B * ((H * W + kSmallGFP - 1) / kSmallGFP) : 0;
-    hipLaunchKernelGGL((warp_bwd_small_kernel<BORDER>), dim3((unsigned)(ngx + ngf)), dim3(kSmallNT), 0, s, x, flow,
-                       fbs, gout, gx, gflow, B, C, H, W, ngx);
-    return;
-  }
-  // binned gather (default with a workspace; usf_set_variant(2, 6) requires one)
+  // binned gather (default with a workspace; usf_set_variant(2, 2) requires one)
   // (bin entries pack (py, px) into 16-bit halves)
-  if (gx && ws && ws_bytes >= bin_layout(B, H, W).total && (v < 0 || v == 6) && H < 32768 && W < 65536) {
+  if (gx && ws && ws_bytes >= bin_layout(B, H, W).total && (v < 0 || v == 2) && H < 32768 && W < 65536) {
     bwd_bins<BORDER>(x, flow, fbs, gout, gx, gflow, B, C, H, W, ws, s);
     return;
   }
-  // usf_set_variant(2, 4): deterministic gather for grad_x. Measured against the
-  // lane-merged scatter at the decoder's batch-16 shapes (profiles/ab_r01/
-  // warp_gather.json): faster for near-zero flows (L4 53 vs 81 us, L1 21 vs
-  // 28 us), slower for +-2 px fields at L2/L3 (60 vs 51, 98 vs 90 us) and for
-  // +-8 px fields everywhere (most sources are scatter outliers), so it is
-  // opt-in.
-  if (gx && v == 4) {
-    const long runs64g = (long)B * ((H * W + 63) / 64);
-    const int csg = (runs64g >= 96 && C >= 4) ? 4 : pick_cs(B, C, H * W);
-    switch (csg) {
-      case 1: bwd_gather_cs<BORDER, 1>(x, flow, fbs, gout, gx, gflow, B, C, H, W, s); break;
-      case 4: bwd_gather_cs<BORDER, 4>(x, flow, fbs, gout, gx, gflow, B, C, H, W, s); break;
-      case 16: bwd_gather_cs<BORDER, 16>(x, flow, fbs, gout, gx, gflow, B, C, H, W, s); break;
-      default: bwd_gather_cs<BORDER, 64>(x, flow, fbs, gout, gx, gflow, B, C, H, W, s); break;
-    }
-    return;
-  }
-  // the scatter variants accumulate into gx: zero it first (gx is overwritten either way)
+  // the scatters accumulate into gx: zero it first (gx is overwritten either way)
   if (gx) (void)zero_fill(gx, sizeof(float) * (size_t)B * C * H * W, s);
-  // pixel-pair scatter: variant 5, and the default for large levels. Measured at
+  // pixel-pair scatter: variant 1, and the default for large levels. Measured at
   // batch 16 (profiles/ab_r01/warp_pairs.json, grad_x + grad_flow): L4 67 vs
   // 82 us (zero flow), 50 vs 60 (constant sub-pixel), equal for +-2 / +-8 px
   // fields; at L2 it halves the workgroups and is slower (52 vs 31 us).
   const bool pair_default = v < 0 && (long)W * ((H + 1) / 2) >= 4096 && C >= 4;
-  if (gx && (v == 5 || pair_default)) {
+  if (gx && (v == 1 || pair_default)) {
     const long runs64p = (long)B * ((W * ((H + 1) / 2) + 63) / 64);
     const int csp = (runs64p >= 96 && C >= 4) ? 4 : pick_cs(B, C, W * ((H + 1) / 2));
     switch (csp) {
@@ -1675,13 +1111,13 @@ void bwd_launch_pad(const float* x, const float* flow, long long fbs, const floa
     }
     return;
   }
-  // Default: CS = 4 (each wave one 64-pixel run of one channel, so an atomic
-  // wave-instruction covers one contiguous row piece) whenever that still gives
-  // ~100 workgroups; narrower pixel runs (CS 16/64) only for the tiny levels.
-  // tools/wbench.py: L3 48 vs 61 us, L2 35 vs 57 us (CS 4 vs 16); L1 (8x26,
-  // 32 workgroups at CS 4) 26 us at CS 64 vs 44 us.
+  // Per-pixel scatter: CS = 4 (each wave one 64-pixel run of one channel, so an
+  // atomic wave-instruction covers one contiguous row piece) whenever that still
+  // gives ~100 workgroups; narrower pixel runs (CS 16/64) only for the tiny
+  // levels. tools/wbench.py: L3 48 vs 61 us, L2 35 vs 57 us (CS 4 vs 16); L1
+  // (8x26, 32 workgroups at CS 4) 26 us at CS 64 vs 44 us.
   const long runs64 = (long)B * ((H * W + 63) / 64);
-  const int cs = v == 2 ? 4 : v == 3 ? 1 : (runs64 >= 96 && C >= 4) ? 4 : pick_cs(B, C, H * W);
+  const int cs = (runs64 >= 96 && C >= 4) ? 4 : pick_cs(B, C, H * W);
   switch (cs) {
     case 1: bwd_launch_cs<BORDER, 1>(x, flow, fbs, gout, gx, gflow, B, C, H, W, s); break;
     case 4: bwd_launch_cs<BORDER, 4>(x, flow, fbs, gout, gx, gflow, B, C, H, W, s); break;

@@ -225,6 +225,14 @@ def clear_persistent_workspaces() -> None:
     _PERSIST.clear()
 
 
+# The largest level (H*W pixels) that takes the persistent two-launch warp
+# backward; larger ones take the four-launch form (None: every level). Chosen by
+# the in-step time of the training step (tools/instep_ab.py, same process,
+# alternating, 4 rounds; profiles/ab_r06/warp_form_instep.json): KITTI L3
+# (32x104) 34.3 us persistent vs 38.7 four-launch, L4 (64x208) 65.2 vs 61.2.
+WARP_PERSIST_MAX_PIXELS: int | None = 8192
+
+
 def warp_backward(
     x: torch.Tensor,
     flow: torch.Tensor,
@@ -264,6 +272,8 @@ def warp_backward(
     # (the C ABI's limits of the persistent form: a 32-bit dirty mask of channel
     # groups, packed (y, x), both count buffers under 32-bit byte offsets)
     persist = need_x and C <= 256 and H < 32768 and W < 65536 and 8 * B * (H + 1) * (W + 1) < 2 ** 31
+    if WARP_PERSIST_MAX_PIXELS is not None and H * W > WARP_PERSIST_MAX_PIXELS:
+        persist = False
     with torch.cuda.device(x.device):
         if persist:
             nws = int(lib.usf_warp_bwd_persist_workspace(B, C, H, W))

@@ -4,7 +4,9 @@ kernels, plus the reference's grid helpers and occlusion estimators.
 * ``flow_warp(x, flow12, pad="border", mode="bilinear")`` (warp_utils.py:97-106)
   — one fused HIP kernel per direction: no CPU ``mesh_grid`` + H2D copy
   (:100), no normalised grid tensor, no ``grid_sample`` launch. Backward
-  returns grad_x (fp32 atomics) only when x requires grad and grad_flow only
+  returns grad_x only when x requires grad -- the binned gather of
+  ``ops.warp_backward`` (every target cell sums its source pixels in a fixed
+  order; fp32 atomics only for pixels beyond 4 per cell) -- and grad_flow only
   when the flow does (``ctx.needs_input_grad``); the loss warps of
   flow_loss.py:130-131 therefore skip grad_x entirely.
 * ``mesh_grid`` / ``norm_grid`` (:7-23) keep their reference semantics
@@ -12,11 +14,12 @@ kernels, plus the reference's grid helpers and occlusion estimators.
   requested device instead of always on the CPU.
 * ``get_corresponding_map`` / ``get_occu_mask_backward`` (:26-94, :120-126)
   run the HIP forward-splat kernel (``usf_splat_map_f32`` /
-  ``usf_occ_backward_f32``: reduce-by-key fp32 atomics, threshold fused in
-  place) instead of ~20 torch ops and an int64 ``scatter_add_``;
-  ``get_occu_mask_bidirection`` (:109-117) is the HIP zeros-padded warp plus
-  elementwise torch ops. No gradient flows through the masks (the reference
-  thresholds them).
+  ``usf_occ_backward_persist_f32``: reduce-by-key fp32 atomics into a
+  persistent map, then a threshold pass that re-zeroes it) instead of ~20
+  torch ops and an int64 ``scatter_add_``; ``get_occu_mask_bidirection``
+  (:109-117) is one kernel (``usf_occ_bidirection_f32``: the zeros-padded
+  warp, the consistency test and the threshold). No gradient flows through
+  the masks (the reference thresholds them).
 """
 from __future__ import annotations
 
