@@ -941,11 +941,14 @@ void bin_pass_cs(const float* x, const float* flow, long long fbs, const float* 
 }
 
 // The gather pass's grid: 32 x 8 target tiles x B x channel groups (multiples
-// of kGatherCH) until ~1024 workgroups, i.e. >= 16 channels per workgroup
-// wherever the grid allows (L3: 43.3 -> 38.3 us against ~2048;
-// profiles/ab_r02/warp_bins_ab.json).
+// of kGatherCH) until ~512 workgroups. Round 2 chose ~1024 against ~2048 by
+// warm replay (L3: 43.3 -> 38.3 us, profiles/ab_r02/warp_bins_ab.json); round
+// 6 compared 512 / 1024 / 2048 by in-step time inside the training step
+// (tools/instep_ab.py, profiles/ab_r06/instep_knobs.json): at KITTI L4 (896
+// tiles x samples) one group of 32 channels instead of two of 16 reads each
+// cell's metadata once: 58.3 vs 62.8 us; L1-L3 within the run-to-run spread.
 #ifndef USF_BIN_WGS
-#define USF_BIN_WGS 1024
+#define USF_BIN_WGS 512
 #endif
 struct GatherGrid {
   int tiles_x, ntiles, cper, zg;
