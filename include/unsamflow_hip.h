@@ -26,6 +26,8 @@
  *   usf_occ_backward_f32 / usf_occ_backward_persist_f32
  *                     <- get_occu_mask_backward (warp_utils.py:120-126),
  *                        caller losses/flow_loss.py:101-103 (occ_from_back)
+ *   usf_occ_vis_pair_persist_f32 <- both directions' 1 - get_occu_mask_backward
+ *                        at once (losses/flow_loss.py:101-103)
  *   usf_occ_bidirection_f32 <- get_occu_mask_bidirection (warp_utils.py:109-117),
  *                        caller losses/flow_loss.py:104-107 (occ_from_back = false)
  *   usf_photo_loss_*  <- the per-scale warp + loss_photomatric composition of
@@ -232,6 +234,19 @@ int usf_occ_backward_f32(const float* flow21, long long flow_bstride, float* occ
  * and zeroes it again, so no fill runs per call (graph-replay safe). One
  * stream at a time per map. occ: [B,1,H,W] dense, overwritten. */
 int usf_occ_backward_persist_f32(const float* flow21, long long flow_bstride, float* occ, float* map,
+                                 long long map_bytes, int B, int H, int W, float th, void* stream);
+
+/* Both directions of the with_bk loss's visibility masks in two launches
+ * (losses/flow_loss.py:101-103: vis_mask1 = 1 - get_occu_mask_backward(
+ * top_flow[:, 2:], 0.2), vis_mask2 = 1 - get_occu_mask_backward(top_flow[:, :2],
+ * 0.2)): one splat over both halves of the dense [B,4,H,W] flow4 (batch stride
+ * 4*H*W) into the persistent map (a caller-owned buffer of >= 8*B*H*W bytes,
+ * ZERO when first passed, re-zeroed by the call), then one threshold pass.
+ * vis: [2,B,1,H,W] dense, overwritten: vis[0] = vis_mask1, vis[1] = vis_mask2
+ * (1 or 0; masks equal get_occu_mask_backward's except where a splat sum lies
+ * within fp32 rounding of th, whose summation order is not fixed). One stream
+ * at a time per map. */
+int usf_occ_vis_pair_persist_f32(const float* flow4, long long flow_bstride, float* vis, float* map,
                                  long long map_bytes, int B, int H, int W, float th, void* stream);
 
 /* Forward-backward consistency occlusion mask (get_occu_mask_bidirection,

@@ -35,7 +35,7 @@ def test_header_declares_the_abi():
          "usf_corr_bwd_ex_scratch",
          "usf_warp_fwd_f32", "usf_warp_bwd_f32", "usf_warp_bwd_ex_f32", "usf_warp_bwd_workspace",
          "usf_warp_bwd_persist_f32", "usf_warp_bwd_persist_workspace",
-         "usf_splat_map_f32", "usf_occ_backward_f32", "usf_occ_backward_persist_f32",
+         "usf_splat_map_f32", "usf_occ_backward_f32", "usf_occ_backward_persist_f32", "usf_occ_vis_pair_persist_f32",
          "usf_occ_bidirection_f32",
          "usf_photo_loss_partials", "usf_photo_loss_fwd_f32", "usf_photo_loss_pair_fwd_f32",
          "usf_photo_loss_bwd_f32",
@@ -110,6 +110,9 @@ def test_no_torch_types_in_abi():
         (lambda L: L.usf_occ_backward_persist_f32(1, 32, 16, 16, 60, 1, 4, 4, 0.2, None), "separate buffer"),
         (lambda L: L.usf_occ_backward_persist_f32(1, 32, 16, 16, 64, 1, 4, 4, 0.2, None), "separate buffer"),
         (lambda L: L.usf_warp_bwd_persist_f32(1, 1, 32, 1, 1, 1, 16, 64, 1, 3, 4, 4, 1, None), "persistent workspace"),
+        (lambda L: L.usf_occ_vis_pair_persist_f32(1, 80, 16, 32, 1 << 20, 2, 4, 4, 0.2, None), "dense [B,4,H,W]"),
+        (lambda L: L.usf_occ_vis_pair_persist_f32(1, 64, 16, 32, 100, 2, 4, 4, 0.2, None), "separate buffer"),
+        (lambda L: L.usf_occ_vis_pair_persist_f32(1, 64, None, 32, 1 << 20, 2, 4, 4, 0.2, None), "null pointer"),
         (lambda L: L.usf_warp_bwd_persist_f32(1, 1, 32, 1, 1, 1, 16, 1 << 40, 1, 300, 4, 4, 1, None), "C=300"),
         # both count buffers of the persistent form must stay under 32-bit byte offsets
         (lambda L: L.usf_warp_bwd_persist_f32(1, 1, 8192, 1, 16, 1, 16, 1 << 60, 70000, 4, 64, 64, 1, None), "2^31"),

@@ -418,6 +418,48 @@ def test_occlusion_vs_oracle_full_size(hip_device, shape, scale):
     assert abs(float(rel.sum()) - float(cmap_ref.sum())) < 1e-3 * max(1.0, float(cmap_ref.sum()))
 
 
+@pytest.mark.parametrize("name", golden_files("occ_"))
+def test_occ_vis_pair_vs_reference_golden(hip_device, name):
+    """ops.occ_vis_pair (usf_occ_vis_pair_persist_f32: both directions' 1 -
+    get_occu_mask_backward from one [B,4,H,W] flow) against the reference's
+    get_occu_mask_backward captures: the captured flow as either half of the
+    4-channel flow, the other half a different field (so each half must come
+    from its own channels)."""
+    from unsamflow_amd import ops
+
+    z = load_golden(name)
+    flow = _occ_flow_dev(z, hip_device).contiguous()
+    other = torch.flip(flow, dims=[-1]).contiguous() * 0.5
+    for first in (True, False):
+        flow4 = torch.cat([other, flow] if first else [flow, other], 1)
+        vis = ops.occ_vis_pair(flow4, 0.2)
+        got = vis[0] if first else vis[1]  # vis[0] from channels 2:4, vis[1] from channels 0:2
+        _assert_occ_equal(1.0 - _np(got), z["occ"], z["map"])
+
+
+@pytest.mark.parametrize("shape,scale", [((8, 256, 832), 4.0), ((8, 256, 832), 0.0), ((2, 64, 208), 30.0),
+                                         ((3, 33, 17), 2.5)])
+def test_occ_vis_pair_vs_oracle_full_size(hip_device, shape, scale):
+    """The loss's call site (both masks of a B=8 [B,4,256,832] flow) vs the oracle,
+    called twice on one persistent map (the threshold pass leaves it zero)."""
+    from oracle.torch_ref import oracle_corresponding_map, oracle_occu_mask_backward
+    from unsamflow_amd import ops
+
+    B, H, W = shape
+    f4 = torch.from_numpy(hashrng.symmetric((B, 4, H, W), 9200 + H, scale)) if scale else torch.zeros(B, 4, H, W)
+    ys, xs = torch.meshgrid(torch.arange(H), torch.arange(W), indexing="ij")
+    grid = torch.stack([xs, ys], 0).float().expand(B, 2, H, W)
+    for _ in range(2):
+        vis = ops.occ_vis_pair(f4.to(hip_device), 0.2)
+        for d, half in ((0, f4[:, 2:]), (1, f4[:, :2])):
+            ref = oracle_occu_mask_backward(half.contiguous(), 0.2)
+            cmap_ref = oracle_corresponding_map(grid + half).numpy()
+            _assert_occ_equal(1.0 - _np(vis[d]), ref.numpy(), cmap_ref)
+    torch.cuda.synchronize()
+    ws, _ = ops._PERSIST[(hip_device.index, "occ_vis_pair", (B, H, W))]
+    assert int(torch.count_nonzero(ws)) == 0
+
+
 @pytest.mark.parametrize("shape,split", [((16, 192, 4, 13), False), ((16, 128, 8, 26), False),
                                          ((8, 96, 16, 52), True), ((3, 100, 5, 9), False),
                                          ((4, 512, 4, 13), True)])

@@ -26,7 +26,7 @@ SITES += [("warp_bwd", (DB, C, H, W, "border", True, True)) for C, H, W in KITTI
 SITES += [("warp_fwd", (8, 3, 256, 832, "border")), ("warp_bwd", (8, 3, 256, 832, "border", False, True))]
 SITES += [("convex_up", (DB, H, W, 4)) for _, H, W in KITTI]
 SITES += [("convex_up_bwd", (DB, H, W, 4)) for _, H, W in KITTI]
-SITES += [("occ_bwd", (8, 1, 256, 832)), ("area_pyramid", (8, 3, 256, 832))]
+SITES += [("occ_bwd", (8, 1, 256, 832)), ("occ_vis_pair", (8, 1, 256, 832)), ("area_pyramid", (8, 3, 256, 832))]
 SITES += [("photo_fwd", (8, 3, 256 >> i, 832 >> i, "border")) for i in range(4)]
 SITES += [("photo_fwd_grad", (8, 3, 256 >> i, 832 >> i, "border")) for i in range(4)]
 SITES += [("photo_pair_grad", (8, 3, 256 >> i, 832 >> i, "border")) for i in range(4)]

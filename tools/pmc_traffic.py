@@ -117,6 +117,8 @@ def main():
             alg = int(4 * B * C * H * W * (1 + 1 / 4 + 1 / 16 + 1 / 64))
         elif op == "occ_bwd":
             alg = 4 * B * H * W * 3  # flow in, mask out (ops.occ_backward)
+        elif op == "occ_vis_pair":
+            alg = 4 * B * H * W * 6  # 4-channel flow in, two masks out (ops.occ_vis_pair)
         elif op == "photo_fwd":
             alg = 4 * B * H * W * (2 * C + 3)
         elif op == "photo_fwd_grad":

@@ -36,7 +36,7 @@ def site_list(ops):
             out += [(op, (8, 3, H, W, "border")) for H, W in SCALES]
         elif op == "photo_bwd":
             out += [(op, (8, 2, H, W)) for H, W in SCALES]
-        elif op == "occ_bwd":
+        elif op in ("occ_bwd", "occ_vis_pair"):
             out += [(op, (8, 1, 256, 832))]
         elif op in ("convex_up", "convex_up_bwd"):
             out += [(op, (DB, H, W, 4)) for _, H, W in KITTI]
@@ -80,6 +80,8 @@ def alg_bytes(op, key):
         return 4 * B * H * W * (2 * C + 4 + 2 + (8 if op == "photo_pair_grad" else 0))
     if op == "occ_bwd":
         return 4 * B * H * W * 3
+    if op == "occ_vis_pair":
+        return 4 * B * H * W * 6
     if op == "upsample":
         return 4 * B * C * H * W * 5  # read x, write the 4x larger output
     if op == "upsample_bwd":

@@ -76,6 +76,11 @@ _SIGNATURES = {
         + [ctypes.c_float, ctypes.c_void_p],
         ctypes.c_int,
     ),
+    "usf_occ_vis_pair_persist_f32": (
+        [_c_float_p, ctypes.c_longlong, _c_float_p, _c_float_p, ctypes.c_longlong] + [ctypes.c_int] * 3
+        + [ctypes.c_float, ctypes.c_void_p],
+        ctypes.c_int,
+    ),
     "usf_splat_map_f32": (
         [_c_float_p, ctypes.c_longlong, _c_float_p] + [ctypes.c_int] * 4 + [ctypes.c_void_p],
         ctypes.c_int,

@@ -397,6 +397,35 @@ int usf_occ_backward_persist_f32(const float* flow21, long long flow_bstride, fl
   return finish(fn, e, (hipStream_t)stream);
 }
 
+int usf_occ_vis_pair_persist_f32(const float* flow4, long long flow_bstride, float* vis, float* map,
+                                 long long map_bytes, int B, int H, int W, float th, void* stream) {
+  clear_error();
+  const char* fn = "usf_occ_vis_pair_persist_f32";
+  if (!check_dims(fn, B, 4, H, W)) return USF_EINVAL;
+  if (!flow4 || !vis) {
+    set_error("%s: null pointer", fn);
+    return USF_EINVAL;
+  }
+  if (B > 1 && flow_bstride != 4LL * H * W) {
+    set_error("%s: flow4 must be a dense [B,4,H,W] tensor (batch stride %lld != 4*H*W)", fn, flow_bstride);
+    return USF_EINVAL;
+  }
+  if (!map || map_bytes < 8LL * B * H * W || map == vis) {
+    set_error("%s: map must be a separate buffer of >= 8*B*H*W = %lld bytes (got %lld)", fn, 8LL * B * H * W,
+              map_bytes);
+    return USF_EINVAL;
+  }
+  if (2LL * B * H * W >= (1LL << 31)) {
+    set_error("%s: 2*B*H*W beyond 32-bit indexing", fn);
+    return USF_EINVAL;
+  }
+  if (const int pe = pre_check(fn, (hipStream_t)stream)) return pe;
+  hipError_t e = occ_vis_pair_persist_launch(flow4, vis, map, B, H, W, th, (hipStream_t)stream);
+  if (e == hipSuccess && sync_check_on((hipStream_t)stream))
+    e = zero_check_launch(map, 8LL * B * H * W, (hipStream_t)stream);
+  return finish(fn, e, (hipStream_t)stream);
+}
+
 int usf_occ_bidirection_f32(const float* flow12, long long flow12_bstride, const float* flow21,
                             long long flow21_bstride, float* occ, int B, int H, int W, float scale,
                             float bias, void* stream) {

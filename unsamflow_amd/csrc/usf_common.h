@@ -119,6 +119,8 @@ hipError_t occ_backward_launch(const float* flow, long long flow_bstride, float*
                                int W, float th, hipStream_t s);
 hipError_t splat_scatter(const float* flow, long long flow_bstride, float* map, int B, int H, int W,
                          bool absolute, hipStream_t s);
+hipError_t occ_vis_pair_persist_launch(const float* flow4, float* vis, float* map, int B, int H, int W, float th,
+                                      hipStream_t s);
 hipError_t occ_backward_persist_launch(const float* flow, long long flow_bstride, float* occ, float* map, int B,
                                        int H, int W, float th, hipStream_t s);
 hipError_t occ_bidirection_launch(const float* flow12, long long bs12, const float* flow21, long long bs21,

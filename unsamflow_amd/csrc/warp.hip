@@ -1277,6 +1277,26 @@ __global__ __launch_bounds__(256) void occ_threshold_kernel(float* m, float* occ
   occ[i] = fminf(fmaxf(v, 0.f), 1.f) < th ? 1.f : 0.f;
 }
 
+// Both directions of a with_bk loss at once (usf_occ_vis_pair_persist_f32):
+// the splat map is interleaved [B][2][H][W] (half j = 0: the splat of
+// flow12 = top[:, :2], j = 1: of flow21 = top[:, 2:]), and the threshold pass
+// writes the visibility masks the loss uses, 1 - occ, direction-major:
+// vis[0][b] = 1 - occ(flow21) (flow_loss.py:102 vis_mask1), vis[1][b] =
+// 1 - occ(flow12) (:103 vis_mask2), each a contiguous [B,1,H,W]; the map is
+// re-zeroed as read (its only reader).
+__global__ __launch_bounds__(256) void occ_vis_pair_kernel(float* __restrict__ m, float* __restrict__ vis, int HW,
+                                                           int B, float th) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  const long long n = 2LL * B * HW;
+  if (i >= n) return;
+  const int b2 = (int)(i / HW), p = (int)(i - (long long)b2 * HW);
+  const int b = b2 >> 1, j = b2 & 1;
+  const float v = m[i];
+  m[i] = 0.f;
+  const float occ = fminf(fmaxf(v, 0.f), 1.f) < th ? 1.f : 0.f;
+  vis[((long long)(1 - j) * B + b) * HW + p] = 1.f - occ;
+}
+
 }  // namespace
 
 int device_errors(hipStream_t s, bool clear) {
@@ -1393,6 +1413,19 @@ hipError_t occ_backward_persist_launch(const float* flow, long long fbs, float* 
   if (e != hipSuccess) return e;
   const long long n = (long long)B * H * W;
   hipLaunchKernelGGL(occ_threshold_kernel<true>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, map, occ, n,
+                     th);
+  return hipGetLastError();
+}
+
+hipError_t occ_vis_pair_persist_launch(const float* flow4, float* vis, float* map, int B, int H, int W, float th,
+                                      hipStream_t s) {
+  // a dense [B,4,H,W] flow is a [2B,2,H,W] batch of (flow12, flow21) pairs: one
+  // splat launch over 2B samples fills the interleaved map
+  const long long HW = (long long)H * W;
+  hipError_t e = splat_scatter(flow4, 2 * HW, map, 2 * B, H, W, false, s);
+  if (e != hipSuccess) return e;
+  const long long n = 2LL * B * HW;
+  hipLaunchKernelGGL(occ_vis_pair_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, map, vis, (int)HW, B,
                      th);
   return hipGetLastError();
 }

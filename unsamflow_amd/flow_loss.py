@@ -115,6 +115,7 @@ class unFlowLoss(nn.Module):  # noqa: N801 (reference name)
         # warp -- e.g. the CPU oracle -- keeps the torch composition below)
         self.fused = warp_fn is None and fused_photometric
         self.occ_backward = occ_backward_fn or warp_utils.get_occu_mask_backward
+        self.lib_occ = occ_backward_fn is None  # the library's masks: both directions in one call
         self.occ_bidir = occ_bidir_fn or (lambda f12, f21: warp_utils.get_occu_mask_bidirection(f12, f21))
 
     def _fused_photometric(self, flow) -> bool:
@@ -162,17 +163,36 @@ class unFlowLoss(nn.Module):  # noqa: N801 (reference name)
         pyr2 = self._image_pyramid(im2_origin, sizes) if pyr1 is not None else None
         top = pyramid_flows[0]
         scale = min(*top.shape[-2:])
-        if c.occ_from_back:
+        vis = None
+        if c.occ_from_back and self.lib_occ and top.is_cuda:
+            # both masks from one HIP call (ops.occ_vis_pair): vis[0] = vis1, vis[1] = vis2
+            from . import ops
+
+            vis = ops.occ_vis_pair(top, th=0.2)
+            vis1, vis2 = vis[0], vis[1]
+        elif c.occ_from_back:
             vis1 = 1 - self.occ_backward(top[:, 2:], th=0.2)
             vis2 = 1 - self.occ_backward(top[:, :2], th=0.2)
         else:
             vis1 = 1 - self.occ_bidir(top[:, :2], top[:, 2:])
             vis2 = 1 - self.occ_bidir(top[:, 2:], top[:, :2])
         vis1_pyr, vis2_pyr = [vis1], [vis2]
-        for f in pyramid_flows[1:5]:
+        for i, f in enumerate(pyramid_flows[1:5], start=1):
+            # (the reference also resizes the masks of scales it does not use;
+            # only scales with a photometric weight read them)
+            if occ_aware and c.w_ph_scales[i] <= 0:
+                vis1_pyr.append(None)
+                vis2_pyr.append(None)
+                continue
             hw = tuple(f.shape[-2:])
-            vis1_pyr.append(F.interpolate(vis1, hw, mode="nearest"))
-            vis2_pyr.append(F.interpolate(vis2, hw, mode="nearest"))
+            if vis is not None:  # both directions in one nearest resize
+                B, _, H, W = top.shape
+                v = F.interpolate(vis.view(2 * B, 1, H, W), hw, mode="nearest").view(2, B, 1, *hw)
+                vis1_pyr.append(v[0])
+                vis2_pyr.append(v[1])
+            else:
+                vis1_pyr.append(F.interpolate(vis1, hw, mode="nearest"))
+                vis2_pyr.append(F.interpolate(vis2, hw, mode="nearest"))
 
         zero = torch.zeros((), dtype=torch.float32, device=dev)  # a fill, not an H2D copy (graph-capturable)
         warp_losses, smooth_losses = [], []

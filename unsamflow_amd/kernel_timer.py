@@ -199,6 +199,14 @@ def site_launcher(op: str, key, device, seed: int = 0):
         coef = torch.rand(3 * ndir, device=device, generator=g)
         gl = torch.ones(ndir, device=device)
         return lambda: ops.photo_loss_backward(basis, coef, gl)
+    if op == "occ_vis_pair":  # both directions of the loss's masks from a [B,4,H,W] flow
+        B, _, H, W = key[:4]
+        yy = torch.linspace(0, 6.2832, H, device=device).view(1, 1, H, 1)
+        xx = torch.linspace(0, 6.2832, W, device=device).view(1, 1, 1, W)
+        ph = torch.rand(B, 2, 1, 1, device=device, generator=g) * 6.2832
+        f2 = torch.sin(2 * xx + ph) + torch.cos(3 * yy - ph)
+        flow4 = torch.cat([f2, -f2], 1).contiguous()
+        return lambda: ops.occ_vis_pair(flow4, 0.2)
     if op in ("occ_bwd", "splat", "photo_fwd", "photo_fwd_grad", "photo_pair", "photo_pair_grad"):
         B, C, H, W = key[:4]
         yy = torch.linspace(0, 6.2832, H, device=device).view(1, 1, H, 1)

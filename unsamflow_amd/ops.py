@@ -336,6 +336,32 @@ def occ_backward(flow21: torch.Tensor, th: float = 0.2) -> torch.Tensor:
     return out
 
 
+def occ_vis_pair(flow4: torch.Tensor, th: float = 0.2) -> torch.Tensor:
+    """Both visibility masks of a with_bk loss at once (flow_loss.py:101-103):
+    ``vis[0] = 1 - get_occu_mask_backward(flow4[:, 2:], th)``, ``vis[1] = 1 -
+    get_occu_mask_backward(flow4[:, :2], th)`` -> [2,B,1,H,W] (each half a
+    contiguous [B,1,H,W]): one splat launch over both flow halves into a
+    persistent interleaved map and one threshold pass (usf_occ_vis_pair_persist_f32)
+    instead of two splats, two thresholds and two ``1 - occ`` passes."""
+    _require_device_f32("flow4", flow4)
+    if flow4.dim() != 4 or flow4.shape[1] != 4:
+        raise ValueError(f"flow4 must be [B,4,H,W], got {tuple(flow4.shape)}")
+    f = flow4.contiguous()
+    B, _, H, W = f.shape
+    vis = torch.empty((2, B, 1, H, W), device=f.device, dtype=torch.float32)
+    lib = _lib.load()
+    with torch.cuda.device(f.device):
+        nmap = 8 * B * H * W
+        ws = persistent_workspace(f.device, "occ_vis_pair", (B, H, W), nmap)
+        with _kt.timed("occ_vis_pair", (B, 1, H, W), f.device, 4 * B * H * W * 6):
+            rc = lib.usf_occ_vis_pair_persist_f32(f.data_ptr(), 4 * H * W, vis.data_ptr(), ws.data_ptr(), nmap, B, H,
+                                                  W, float(th), _lib.stream_handle(f.device))
+    if rc != 0:
+        _drop_workspace(f.device, "occ_vis_pair", (B, H, W))
+    _lib.check(rc, "usf_occ_vis_pair_persist_f32")
+    return vis
+
+
 def occ_bidirection(flow12: torch.Tensor, flow21: torch.Tensor, scale: float = 0.01, bias: float = 0.5
                     ) -> torch.Tensor:
     """Occlusion mask get_occu_mask_bidirection (warp_utils.py:109-117) -> [B,1,H,W] float, one kernel."""
