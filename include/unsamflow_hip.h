@@ -291,6 +291,31 @@ int usf_photo_loss_pair_fwd_f32(const float* im1, const float* im2, const float*
                                 int H, int W, int pad_mode, float w_l1, float w_ssim,
                                 void* stream);
 
+/* The with_bk pairs of up to 4 loss scales in ONE launch (+ one final
+ * reduction): scale k (largest first) is usf_photo_loss_pair_fwd_f32's call
+ * with im1[k], im2[k], mask1[k], mask2[k], flow[k] (batch stride
+ * flow_bstride[k]), H[k] x W[k]; the small scales' strips fill the chip's tail
+ * instead of each paying a launch and a drain (flow_loss.py:120-148, the scale
+ * loop). Arrays are HOST arrays of nscale entries (1 <= nscale <= 4) holding
+ * device pointers. partials: usf_photo_loss_pyramid_partials(nscale, H, W, B)
+ * floats; out: 6 * nscale floats ({L, c_l1, c_ssim} per direction per scale);
+ * grad_basis: NULL (no gradient) or nscale [B,8,H[k],W[k]] buffers. Results
+ * equal nscale separate usf_photo_loss_pair_fwd_f32 calls bit for bit. */
+long long usf_photo_loss_pyramid_partials(int nscale, const int* H, const int* W, int B);
+int usf_photo_loss_pyramid_fwd_f32(int nscale, const float* const* im1, const float* const* im2,
+                                   const float* const* mask1, const float* const* mask2, const float* const* flow,
+                                   const long long* flow_bstride, const int* H, const int* W, float* partials,
+                                   long long partials_floats, float* out, float* const* grad_basis, int B, int C,
+                                   int pad_mode, float w_l1, float w_ssim, void* stream);
+
+/* Its backward, every scale in one launch: grad_flow[k] ([B,4,H[k],W[k]],
+ * overwritten) = per direction d (c_l1 A + c_ssim S) * grad_loss[2 k + d]
+ * from grad_basis[k] and coef = the forward's out. Host arrays of device
+ * pointers, as above. */
+int usf_photo_loss_pyramid_bwd_f32(int nscale, const float* const* grad_basis, const float* coef,
+                                   const float* grad_loss, float* const* grad_flow, const int* H, const int* W, int B,
+                                   void* stream);
+
 /* Backward of usf_photo_loss_fwd_f32 (ndir = 1) or _pair_fwd_f32 (ndir = 2)
  * w.r.t. the flow only (the mask and the images carry no gradient):
  * grad_flow[:, 2d:2d+2] = (c_l1 * A + c_ssim * S) * grad_loss[d] per direction d.

@@ -38,7 +38,8 @@ def test_header_declares_the_abi():
          "usf_splat_map_f32", "usf_occ_backward_f32", "usf_occ_backward_persist_f32", "usf_occ_vis_pair_persist_f32",
          "usf_occ_bidirection_f32",
          "usf_photo_loss_partials", "usf_photo_loss_fwd_f32", "usf_photo_loss_pair_fwd_f32",
-         "usf_photo_loss_bwd_f32",
+         "usf_photo_loss_bwd_f32", "usf_photo_loss_pyramid_partials", "usf_photo_loss_pyramid_fwd_f32",
+         "usf_photo_loss_pyramid_bwd_f32",
          "usf_flow_upsample_f32", "usf_flow_upsample_bwd_f32", "usf_area_pyramid_f32",
          "usf_convex_upsample_f32", "usf_convex_upsample_bwd_scratch", "usf_convex_upsample_bwd_f32",
          "usf_set_variant", "usf_device_errors", "usf_stream_copy_f32"]
@@ -120,6 +121,9 @@ def test_no_torch_types_in_abi():
         (lambda L: L.usf_photo_loss_fwd_f32(1, 1, 1, 1, 32, 1, 1, 1, 1, 3, 4, 4, 9, 0.15, 0.85, None), "pad_mode 9"),
         (lambda L: L.usf_photo_loss_fwd_f32(1, None, 1, 1, 32, 1, 1, None, 1, 3, 4, 4, 1, 0.15, 0.85, None), "null input"),
         (lambda L: L.usf_photo_loss_bwd_f32(1, None, 1, 1, 1, 4, 4, 1, None), "null pointer"),
+        (lambda L: L.usf_photo_loss_pyramid_fwd_f32(5, 1, 1, 1, 1, 1, 1, 1, 1, 1, 0, 1, None, 1, 3, 1, 0.15, 0.85,
+                                                     None), "nscale 5"),
+        (lambda L: L.usf_photo_loss_pyramid_bwd_f32(0, 1, 1, 1, 1, 1, 1, 1, None), "nscale 0"),
         (lambda L: L.usf_area_pyramid_f32(1, 1, 1, 1, 1, 3, 12, 16, None), "multiples of 8"),
         (lambda L: L.usf_area_pyramid_f32(1, None, 1, 1, 1, 3, 16, 16, None), "null pointer"),
         (lambda L: L.usf_photo_loss_bwd_f32(1, 1, 1, 1, 0, 4, 4, 1, None), "non-positive"),

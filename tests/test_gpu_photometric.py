@@ -148,3 +148,34 @@ def test_photometric_forward_only_matches_grad_forward(hip_device):
     b, none = ops.photo_loss_forward(src, tgt, mask, flow, "border", need_grad=False)
     assert none is None and basis.shape == (B, 4, H, W)
     np.testing.assert_allclose(a.cpu().numpy(), b.cpu().numpy(), rtol=1e-6, atol=0)
+
+
+@pytest.mark.parametrize("pad", ["border", "zeros"])
+@pytest.mark.parametrize("B,C,sizes", [(8, 3, [(256, 832), (128, 416), (64, 208), (32, 104)]),
+                                        (2, 3, [(33, 47), (17, 24)]), (2, 1, [(40, 64), (20, 32), (10, 16)])])
+def test_photometric_pyramid_equals_per_scale_pairs(hip_device, B, C, sizes, pad):
+    """photometric_loss_pyramid (usf_photo_loss_pyramid_{fwd,bwd}_f32: every
+    loss scale in one forward launch and one backward launch) gives the
+    per-scale photometric_loss_pair results bit for bit -- losses and each
+    scale's flow gradient -- at the KITTI loss scales (B=8, 832x256 down to
+    104x32) and odd sizes; the per-scale form is itself checked against the
+    reference composition above."""
+    from unsamflow_amd.photometric import photometric_loss_pair, photometric_loss_pyramid
+
+    flows, i1, i2, m1, m2 = [], [], [], [], []
+    for k, (H, W) in enumerate(sizes):
+        flows.append(torch.from_numpy(hashrng.symmetric((B, 4, H, W), 950 + k, 3.0)).to(hip_device))
+        i1.append(torch.from_numpy(hashrng.uniform((B, C, H, W), 960 + k)).to(hip_device))
+        i2.append(torch.from_numpy(hashrng.uniform((B, C, H, W), 970 + k)).to(hip_device))
+        m1.append((torch.from_numpy(hashrng.uniform((B, 1, H, W), 980 + k)) > 0.2).float().to(hip_device))
+        m2.append((torch.from_numpy(hashrng.uniform((B, 1, H, W), 990 + k)) > 0.2).float().to(hip_device))
+    fa = [f.clone().requires_grad_(True) for f in flows]
+    fb = [f.clone().requires_grad_(True) for f in flows]
+    lp = photometric_loss_pyramid(fa, i1, i2, m1, m2, pad)
+    ref = torch.stack([photometric_loss_pair(f, a, b, x, y, pad) for f, a, b, x, y in zip(fb, i1, i2, m1, m2)])
+    assert torch.equal(lp, ref)
+    wts = torch.arange(1, 2 * len(sizes) + 1, device=hip_device, dtype=torch.float32).view(-1, 2)
+    (lp * wts).sum().backward()
+    (ref * wts).sum().backward()
+    for a, b in zip(fa, fb):
+        assert torch.equal(a.grad, b.grad)

@@ -11,6 +11,7 @@ Usage (GPU box, repo root):
 """
 import argparse
 import ctypes
+import importlib
 import json
 import os
 import statistics
@@ -70,8 +71,10 @@ def main():
         torch.cuda.synchronize()
         ops.clear_persistent_workspaces()  # layouts may differ between builds
         _lib._lib = handles[lp]
-        if name:
-            setattr(ops, name, val)
+        if name:  # an ops global, or module.NAME of another unsamflow_amd module
+            mod, _, attr = name.rpartition(".")
+            target = importlib.import_module("unsamflow_amd." + mod) if mod else ops
+            setattr(target, attr, val)
 
     res = {c: {"ms": [], "sites": {}} for c in configs}
     for c in configs:  # warm every configuration (solver caches, allocator, workspaces)

@@ -94,7 +94,11 @@ def main():
                        "fetch_kib": round(statistics.median(launch[i][1] for launch in fl if len(launch) > i), 1),
                        "write_kib": round(statistics.median(launch[i][1] for launch in wl if len(launch) > i), 1)}
                       for i, nm in enumerate(names)]
-        if op == "photo_bwd":
+        if op in ("photo_pyr_grad", "photo_pyr_bwd"):
+            B, C = key[:2]
+            hw = [(key[i], key[i + 1]) for i in range(2, len(key) - (op == "photo_pyr_grad"), 2)]
+            H, W = hw[0]
+        elif op == "photo_bwd":
             B, ndir, H, W = key
         elif op.startswith("convex_up"):
             B, H, W, f = key
@@ -127,6 +131,10 @@ def main():
             # both directions, every input read once: im1, im2, flow4,
             # both masks; the 8 basis planes written once (ops.photo_loss_pair_forward)
             alg = 4 * B * H * W * (2 * C + 4 + 2 + 8)
+        elif op == "photo_pyr_grad":  # every scale's photo_pair_grad bytes
+            alg = sum(4 * B * h * w * (2 * C + 4 + 2 + 8) for h, w in hw)
+        elif op == "photo_pyr_bwd":  # basis in, grad_flow out, both directions per scale
+            alg = sum(4 * B * h * w * 12 for h, w in hw)
         else:
             alg = 4 * B * H * W * 6 * ndir  # photo_bwd: basis in, grad_flow out
         traffic = fk * 1024 * f_read + wk * 1024 * f_write

@@ -105,6 +105,18 @@ _SIGNATURES = {
         + [ctypes.c_float, ctypes.c_float, ctypes.c_void_p],
         ctypes.c_int,
     ),
+    "usf_photo_loss_pyramid_partials": ([ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int],
+                                        ctypes.c_longlong),
+    "usf_photo_loss_pyramid_fwd_f32": (
+        [ctypes.c_int] + [ctypes.c_void_p] * 8 + [_c_float_p, ctypes.c_longlong, _c_float_p, ctypes.c_void_p]
+        + [ctypes.c_int] * 3 + [ctypes.c_float, ctypes.c_float, ctypes.c_void_p],
+        ctypes.c_int,
+    ),
+    "usf_photo_loss_pyramid_bwd_f32": (
+        [ctypes.c_int, ctypes.c_void_p, _c_float_p, _c_float_p] + [ctypes.c_void_p] * 3 + [ctypes.c_int,
+                                                                                            ctypes.c_void_p],
+        ctypes.c_int,
+    ),
     "usf_photo_loss_bwd_f32": (
         [_c_float_p] * 4 + [ctypes.c_int] * 4 + [ctypes.c_void_p],
         ctypes.c_int,

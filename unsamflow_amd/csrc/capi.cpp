@@ -511,6 +511,72 @@ int usf_photo_loss_pair_fwd_f32(const float* im1, const float* im2, const float*
                 (hipStream_t)stream);
 }
 
+long long usf_photo_loss_pyramid_partials(int nscale, const int* H, const int* W, int B) {
+  if (nscale < 1 || nscale > 4 || !H || !W || B <= 0) return 0;
+  long long n = 0;
+  for (int k = 0; k < nscale; ++k) {
+    if (H[k] <= 0 || W[k] <= 0) return 0;
+    n += 2LL * photo_partials(B, H[k], W[k]);
+  }
+  return n;
+}
+
+int usf_photo_loss_pyramid_fwd_f32(int nscale, const float* const* im1, const float* const* im2,
+                                   const float* const* mask1, const float* const* mask2, const float* const* flow,
+                                   const long long* flow_bstride, const int* H, const int* W, float* partials,
+                                   long long partials_floats, float* out, float* const* grad_basis, int B, int C,
+                                   int pad_mode, float w_l1, float w_ssim, void* stream) {
+  clear_error();
+  const char* fn = "usf_photo_loss_pyramid_fwd_f32";
+  if (nscale < 1 || nscale > 4 || !im1 || !im2 || !mask1 || !mask2 || !flow || !flow_bstride || !H || !W) {
+    set_error("%s: nscale %d not in [1,4] or a null array", fn, nscale);
+    return USF_EINVAL;
+  }
+  for (int k = 0; k < nscale; ++k) {
+    if (!check_photo(fn, im1[k], im2[k], mask1[k], flow[k], flow_bstride[k], B, C, H[k], W[k], pad_mode))
+      return USF_EINVAL;
+    if (!mask2[k] || (B > 1 && flow_bstride[k] < 4LL * H[k] * W[k])) {
+      set_error("%s: scale %d: null mask2 or flow batch stride %lld < 4*H*W", fn, k, flow_bstride[k]);
+      return USF_EINVAL;
+    }
+    if (grad_basis && !grad_basis[k]) {
+      set_error("%s: scale %d: grad_basis given for some scales only", fn, k);
+      return USF_EINVAL;
+    }
+  }
+  if (!partials || !out || partials_floats < usf_photo_loss_pyramid_partials(nscale, H, W, B)) {
+    set_error("%s: partials of %lld floats < usf_photo_loss_pyramid_partials = %lld, or null out", fn,
+              partials_floats, usf_photo_loss_pyramid_partials(nscale, H, W, B));
+    return USF_EINVAL;
+  }
+  if (const int pe = pre_check(fn, (hipStream_t)stream)) return pe;
+  return finish(fn,
+                photo_pyr_fwd_launch(nscale, im1, im2, mask1, mask2, flow, flow_bstride, H, W, partials, out,
+                                     grad_basis, B, C, pad_mode, w_l1, w_ssim, (hipStream_t)stream),
+                (hipStream_t)stream);
+}
+
+int usf_photo_loss_pyramid_bwd_f32(int nscale, const float* const* grad_basis, const float* coef,
+                                   const float* grad_loss, float* const* grad_flow, const int* H, const int* W, int B,
+                                   void* stream) {
+  clear_error();
+  const char* fn = "usf_photo_loss_pyramid_bwd_f32";
+  if (nscale < 1 || nscale > 4 || !grad_basis || !grad_flow || !H || !W || !coef || !grad_loss || B <= 0) {
+    set_error("%s: nscale %d not in [1,4], B=%d, or a null pointer", fn, nscale, B);
+    return USF_EINVAL;
+  }
+  for (int k = 0; k < nscale; ++k) {
+    if (!check_dims(fn, B, 8, H[k], W[k])) return USF_EINVAL;
+    if (!grad_basis[k] || !grad_flow[k]) {
+      set_error("%s: scale %d: null pointer", fn, k);
+      return USF_EINVAL;
+    }
+  }
+  if (const int pe = pre_check(fn, (hipStream_t)stream)) return pe;
+  return finish(fn, photo_pyr_bwd_launch(nscale, grad_basis, coef, grad_loss, grad_flow, H, W, B, (hipStream_t)stream),
+                (hipStream_t)stream);
+}
+
 int usf_photo_loss_bwd_f32(const float* grad_basis, const float* coef, const float* grad_loss,
                            float* grad_flow, int B, int H, int W, int ndir, void* stream) {
   clear_error();

@@ -504,8 +504,10 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
+// The strip stream of one scale's workgroup blk of nblk (photo_pc_kernel: the
+// whole grid; photo_pyr_kernel: that scale's range of a multi-scale grid).
 template <bool BORDER, bool GRAD, int C>
-__global__ __launch_bounds__(128 * kPairs) __attribute__((amdgpu_waves_per_eu(USF_PHOTO_EU))) void photo_pc_kernel(StripArgs a, float* __restrict__ partials) {
+__device__ __forceinline__ void pc_body(const StripArgs& a, float* __restrict__ partials, int blk, int nblk) {
   __shared__ float lds[kPairs][2][kRing * C * 2 * 64];  // [pair][x,y | gradient state]
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -513,7 +515,7 @@ __global__ __launch_bounds__(128 * kPairs) __attribute__((amdgpu_waves_per_eu(US
   const bool prod = (wave & 1) == 0;
   // workgroup -> (sample, strip row, pair of strip items sharing that row)
   const int npx = kPairs == 1 ? a.ndir * a.nsx : a.ndir == 2 ? a.nsx : (a.nsx + 1) / 2;  // workgroups per strip row
-  const int g = xcd_remap(blockIdx.x, gridDim.x);
+  const int g = xcd_remap(blk, nblk);
   const int gx = g % npx, rest = g / npx;
   const int sy = rest % a.nsy, b = rest / a.nsy;
   const int dirn = kPairs == 1 ? gx % a.ndir : a.ndir == 2 ? pair : 0;
@@ -614,6 +616,123 @@ __global__ __launch_bounds__(128 * kPairs) __attribute__((amdgpu_waves_per_eu(US
   }
 }
 
+template <bool BORDER, bool GRAD, int C>
+__global__ __launch_bounds__(128 * kPairs) __attribute__((amdgpu_waves_per_eu(USF_PHOTO_EU))) void photo_pc_kernel(StripArgs a, float* __restrict__ partials) {
+  pc_body<BORDER, GRAD, C>(a, partials, blockIdx.x, gridDim.x);
+}
+
+// The loss scales of a with_bk step in ONE launch (usf_photo_loss_pyramid_fwd_f32):
+// scale s owns workgroups [start[s], start[s + 1]) -- the largest scale first,
+// so the small scales' few strips fill the chip's tail instead of each paying a
+// launch and a drain of their own.
+constexpr int kMaxScales = 4;
+struct StripPyr {
+  StripArgs sc[kMaxScales];
+  float* part[kMaxScales];
+  int start[kMaxScales + 1];
+};
+
+template <bool BORDER, bool GRAD, int C>
+__global__ __launch_bounds__(128 * kPairs) __attribute__((amdgpu_waves_per_eu(USF_PHOTO_EU))) void photo_pyr_kernel(StripPyr m) {
+  const int blk = blockIdx.x;
+  const int s = (blk >= m.start[1]) + (blk >= m.start[2]) + (blk >= m.start[3]);  // unused scales: start = total
+  pc_body<BORDER, GRAD, C>(m.sc[s], m.part[s], blk - m.start[s], m.start[s + 1] - m.start[s]);
+}
+
+// One block per (direction, scale): photo_final_kernel's fixed-order reduction.
+struct FinPyr {
+  const float* part[kMaxScales];
+  int nblk[kMaxScales];
+  double n1[kMaxScales], n2[kMaxScales], n3[kMaxScales];
+};
+__global__ __launch_bounds__(kFinNT) void photo_pyr_final_kernel(FinPyr f, float* __restrict__ out, float w_l1,
+                                                                 float w_ssim) {
+  const int s = blockIdx.y;
+  // the same code as the single-scale reduction, on this scale's partials (one
+  // block per direction: blockIdx.x) and outputs out[6 s ..]
+  __shared__ double red[3][kFinNT / 64];
+  const int t = threadIdx.x, dirn = blockIdx.x, nblk = f.nblk[s];
+  const float* p = f.part[s] + (size_t)3 * nblk * dirn;
+  double a = 0, b = 0, c = 0;
+  int i = t;
+  for (; i + 3 * kFinNT < nblk; i += 4 * kFinNT) {
+    float v[4][3];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int q = 0; q < 3; ++q) v[j][q] = p[3 * (i + j * kFinNT) + q];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      a += v[j][0];
+      b += v[j][1];
+      c += v[j][2];
+    }
+  }
+  for (; i < nblk; i += kFinNT) {
+    a += p[3 * i];
+    b += p[3 * i + 1];
+    c += p[3 * i + 2];
+  }
+#pragma unroll
+  for (int sh = 32; sh > 0; sh >>= 1) {
+    a += __shfl_xor(a, sh);
+    b += __shfl_xor(b, sh);
+    c += __shfl_xor(c, sh);
+  }
+  if ((t & 63) == 0) {
+    red[0][t >> 6] = a;
+    red[1][t >> 6] = b;
+    red[2][t >> 6] = c;
+  }
+  __syncthreads();
+  if (t == 0) {
+    double s0 = 0, s1 = 0, s2 = 0;
+    for (int w = 0; w < kFinNT / 64; ++w) {
+      s0 += red[0][w];
+      s1 += red[1][w];
+      s2 += red[2][w];
+    }
+    const double n1 = f.n1[s], n2 = f.n2[s], n3 = f.n3[s];
+    const double den = s2 / n3 + 1e-6;
+    const double l1 = n1 > 0 ? s0 / n1 : 0.0, ss = n2 > 0 ? s1 / n2 : 0.0;
+    float* o = out + 6 * s + 3 * dirn;
+    o[0] = (float)((w_l1 * l1 + w_ssim * ss) / den);
+    o[1] = n1 > 0 ? (float)(w_l1 / (n1 * den)) : 0.f;
+    o[2] = n2 > 0 ? (float)(w_ssim / (n2 * den)) : 0.f;
+  }
+}
+
+// The backward of every scale in one launch: blockIdx.z = 2 s + direction.
+struct BwdPyr {
+  const float* basis[kMaxScales];
+  float* gflow[kMaxScales];
+  int HW[kMaxScales];
+};
+__global__ __launch_bounds__(256) void photo_pyr_bwd_kernel(BwdPyr m, const float* __restrict__ coef,
+                                                            const float* __restrict__ gloss) {
+  const int s = blockIdx.z >> 1, dirn = blockIdx.z & 1, b = blockIdx.y;
+  const int HW = m.HW[s];
+  const int i = (blockIdx.x * 256 + threadIdx.x) * 4;
+  if (i >= HW) return;
+  const float gl = gloss[2 * s + dirn];
+  const float k1 = coef[6 * s + 3 * dirn + 1] * gl, k2 = coef[6 * s + 3 * dirn + 2] * gl;
+  const float* a = m.basis[s] + ((size_t)b * 2 + dirn) * 4 * HW;
+  float* o = m.gflow[s] + ((size_t)b * 2 + dirn) * 2 * HW;
+  if ((HW & 3) == 0) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const float4 u = *reinterpret_cast<const float4*>(a + j * HW + i);
+      const float4 v = *reinterpret_cast<const float4*>(a + (2 + j) * HW + i);
+      *reinterpret_cast<float4*>(o + j * HW + i) =
+          make_float4(k1 * u.x + k2 * v.x, k1 * u.y + k2 * v.y, k1 * u.z + k2 * v.z, k1 * u.w + k2 * v.w);
+    }
+  } else {
+    for (int e = i; e < i + 4 && e < HW; ++e)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) o[j * HW + e] = k1 * a[j * HW + e] + k2 * a[(2 + j) * HW + e];
+  }
+}
+
 // Strip heights. Every wave streams R + 4 rows, so a launch takes about
 // (R + 4) steps times the rounds of strips the chip holds: USF_PHOTO_EU / 2
 // wave pairs per SIMD (the pair kernel's registers), 1024 SIMDs. A step of a wave alone on its
@@ -660,6 +779,38 @@ hipError_t pc_launch_c(const StripArgs& sa, int C, dim3 grid, float* partials, h
     hipLaunchKernelGGL((photo_pc_kernel<BORDER, GRAD, 2>), grid, dim3(128 * kPairs), 0, s, sa, partials);
   else
     hipLaunchKernelGGL((photo_pc_kernel<BORDER, GRAD, 1>), grid, dim3(128 * kPairs), 0, s, sa, partials);
+  return hipGetLastError();
+}
+
+// StripArgs of one launch (one scale, ndir directions) and its workgroup count.
+StripArgs strip_args(const PhotoArgs& a, int ndir, unsigned& nwg) {
+  StripArgs sa{};
+  sa.dir[0] = a.dir[0];
+  sa.dir[1] = a.dir[1];
+  sa.fbs = a.fbs;
+  sa.bbs = a.bbs;
+  sa.B = a.B;
+  sa.H = a.H;
+  sa.W = a.W;
+  const StripPlan plan = strip_plan(a.B, a.H, a.W, ndir);
+  sa.R = plan.R;
+  sa.nsx = (a.W + kSO - 1) / kSO;
+  sa.nsy = plan.nsy;
+  sa.ndir = ndir;
+  sa.nitems = ndir * a.B * sa.nsx * sa.nsy;
+  const int npx = kPairs == 1 ? ndir * sa.nsx : ndir == 2 ? sa.nsx : (sa.nsx + 1) / 2;
+  nwg = (unsigned)(a.B * sa.nsy * npx);
+  return sa;
+}
+
+template <bool BORDER, bool GRAD>
+hipError_t pyr_launch_c(const StripPyr& m, int C, dim3 grid, hipStream_t s) {
+  if (C == 3)
+    hipLaunchKernelGGL((photo_pyr_kernel<BORDER, GRAD, 3>), grid, dim3(128 * kPairs), 0, s, m);
+  else if (C == 2)
+    hipLaunchKernelGGL((photo_pyr_kernel<BORDER, GRAD, 2>), grid, dim3(128 * kPairs), 0, s, m);
+  else
+    hipLaunchKernelGGL((photo_pyr_kernel<BORDER, GRAD, 1>), grid, dim3(128 * kPairs), 0, s, m);
   return hipGetLastError();
 }
 
@@ -732,6 +883,68 @@ hipError_t photo_pair_fwd_launch(const float* im1, const float* im2, const float
   a.bbs = 8LL * H * W;
   a.B = B; a.C = C; a.H = H; a.W = W;
   return photo_launch(a, 2, pad_mode, partials, out, w_l1, w_ssim, s);
+}
+
+hipError_t photo_pyr_fwd_launch(int nscale, const float* const* im1, const float* const* im2,
+                                const float* const* mask1, const float* const* mask2, const float* const* flow,
+                                const long long* fbs, const int* H, const int* W, float* partials, float* out,
+                                float* const* basis, int B, int C, int pad_mode, float w_l1, float w_ssim,
+                                hipStream_t s) {
+  if (nscale < 1 || nscale > kMaxScales) return hipErrorInvalidValue;
+  StripPyr m{};
+  FinPyr f{};
+  bool grad = false;
+  unsigned total = 0;
+  long long poff = 0;
+  for (int k = 0; k < nscale; ++k) {
+    PhotoArgs a{};
+    const size_t HW = (size_t)H[k] * W[k];
+    float* bk = basis ? basis[k] : nullptr;
+    a.dir[0] = PhotoDir{im2[k], im1[k], mask1[k], flow[k], bk};
+    a.dir[1] = PhotoDir{im1[k], im2[k], mask2[k], flow[k] + 2 * HW, bk ? bk + 4 * HW : nullptr};
+    a.fbs = fbs[k];
+    a.bbs = 8LL * H[k] * W[k];
+    a.B = B; a.C = C; a.H = H[k]; a.W = W[k];
+    grad = grad || bk != nullptr;
+    unsigned nwg = 0;
+    m.sc[k] = strip_args(a, 2, nwg);
+    m.part[k] = partials + poff;
+    m.start[k] = (int)total;
+    total += nwg;
+    f.part[k] = partials + poff;
+    f.nblk[k] = B * m.sc[k].nsx * m.sc[k].nsy;
+    f.n1[k] = (double)B * C * H[k] * W[k];
+    f.n2[k] = (H[k] >= 3 && W[k] >= 3) ? (double)B * C * (H[k] - 2) * (W[k] - 2) : 0.0;
+    f.n3[k] = (double)B * H[k] * W[k];
+    poff += 2LL * photo_partials(B, H[k], W[k]);
+  }
+  for (int k = nscale; k <= kMaxScales; ++k) m.start[k] = (int)total;
+  for (int k = nscale; k < kMaxScales; ++k) m.sc[k] = m.sc[0];  // never selected (start[k] = total)
+  hipError_t e;
+  const dim3 grid(total);
+  if (pad_mode == 1)
+    e = grad ? pyr_launch_c<true, true>(m, C, grid, s) : pyr_launch_c<true, false>(m, C, grid, s);
+  else
+    e = grad ? pyr_launch_c<false, true>(m, C, grid, s) : pyr_launch_c<false, false>(m, C, grid, s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(photo_pyr_final_kernel, dim3(2, (unsigned)nscale), dim3(kFinNT), 0, s, f, out, w_l1, w_ssim);
+  return hipGetLastError();
+}
+
+hipError_t photo_pyr_bwd_launch(int nscale, const float* const* basis, const float* coef, const float* gloss,
+                                float* const* gflow, const int* H, const int* W, int B, hipStream_t s) {
+  if (nscale < 1 || nscale > kMaxScales) return hipErrorInvalidValue;
+  BwdPyr m{};
+  int hwmax = 0;
+  for (int k = 0; k < nscale; ++k) {
+    m.basis[k] = basis[k];
+    m.gflow[k] = gflow[k];
+    m.HW[k] = H[k] * W[k];
+    hwmax = std::max(hwmax, m.HW[k]);
+  }
+  const dim3 grid((unsigned)((hwmax + 1023) / 1024), (unsigned)B, (unsigned)(2 * nscale));
+  hipLaunchKernelGGL(photo_pyr_bwd_kernel, grid, dim3(256), 0, s, m, coef, gloss);
+  return hipGetLastError();
 }
 
 hipError_t photo_bwd_launch(const float* basis, const float* coef, const float* gloss, float* gflow,

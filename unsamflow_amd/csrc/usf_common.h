@@ -134,6 +134,13 @@ hipError_t photo_pair_fwd_launch(const float* im1, const float* im2, const float
                                  const float* mask2, const float* flow, long long flow_bstride,
                                  float* partials, float* out, float* basis, int B, int C, int H,
                                  int W, int pad_mode, float w_l1, float w_ssim, hipStream_t s);
+hipError_t photo_pyr_fwd_launch(int nscale, const float* const* im1, const float* const* im2,
+                                const float* const* mask1, const float* const* mask2, const float* const* flow,
+                                const long long* fbs, const int* H, const int* W, float* partials, float* out,
+                                float* const* basis, int B, int C, int pad_mode, float w_l1, float w_ssim,
+                                hipStream_t s);
+hipError_t photo_pyr_bwd_launch(int nscale, const float* const* basis, const float* coef, const float* gloss,
+                                float* const* gflow, const int* H, const int* W, int B, hipStream_t s);
 hipError_t photo_bwd_launch(const float* basis, const float* coef, const float* gloss, float* gflow,
                             int B, int H, int W, int ndir, hipStream_t s);
 

@@ -101,6 +101,10 @@ def _default_warp():
     return flow_warp
 
 
+# every weighted loss scale's photometric pair in one launch (photometric_loss_pyramid)
+PHOTO_PYRAMID = True
+
+
 class unFlowLoss(nn.Module):  # noqa: N801 (reference name)
     def __init__(self, cfg, warp_fn: Callable | None = None, occ_backward_fn: Callable | None = None,
                  occ_bidir_fn: Callable | None = None, fused_photometric: bool = True):
@@ -195,11 +199,29 @@ class unFlowLoss(nn.Module):  # noqa: N801 (reference name)
                 vis2_pyr.append(F.interpolate(vis2, hw, mode="nearest"))
 
         zero = torch.zeros((), dtype=torch.float32, device=dev)  # a fill, not an H2D copy (graph-capturable)
+        # with_bk on the library's kernels: every weighted scale's photometric
+        # pair in ONE launch (photometric_loss_pyramid; the per-scale results,
+        # the small scales filling the chip's tail)
+        pyr_losses = {}
+        scales = [i for i, f in enumerate(pyramid_flows) if c.w_ph_scales[i] > 0]
+        if (PHOTO_PYRAMID and c.with_bk and pyr1 is not None and 1 < len(scales) <= 4 and occ_aware
+                and all(self._fused_photometric(pyramid_flows[i]) for i in scales)):
+            from .photometric import photometric_loss_pyramid
+
+            hws = [tuple(pyramid_flows[i].shape[-2:]) for i in scales]
+            lp = photometric_loss_pyramid([pyramid_flows[i] for i in scales], [pyr1[hw] for hw in hws],
+                                          [pyr2[hw] for hw in hws], [vis1_pyr[i] for i in scales],
+                                          [vis2_pyr[i] for i in scales], c.warp_pad, c.w_l1, c.w_ssim)
+            pyr_losses = {i: (lp[k, 0] + lp[k, 1]) / 2.0 for k, i in enumerate(scales)}
         warp_losses, smooth_losses = [], []
         for i, flow in enumerate(pyramid_flows):
             b, _, h, w = flow.size()
             im1_s = im2_s = None
-            if c.w_ph_scales[i] > 0:
+            if i in pyr_losses:
+                warp_losses.append(pyr_losses[i])
+                if pyr1 is not None:
+                    im1_s, im2_s = pyr1[(h, w)], pyr2[(h, w)]
+            elif c.w_ph_scales[i] > 0:
                 if pyr1 is not None:  # F.interpolate(im, (h, w), mode="area") from the HIP pyramid
                     im1_s, im2_s = pyr1[(h, w)], pyr2[(h, w)]
                 else:

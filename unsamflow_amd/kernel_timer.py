@@ -199,6 +199,26 @@ def site_launcher(op: str, key, device, seed: int = 0):
         coef = torch.rand(3 * ndir, device=device, generator=g)
         gl = torch.ones(ndir, device=device)
         return lambda: ops.photo_loss_backward(basis, coef, gl)
+    if op in ("photo_pyr", "photo_pyr_grad", "photo_pyr_bwd"):  # the loss scales in one launch
+        B, C = key[:2]
+        hw = [(key[i], key[i + 1]) for i in range(2, len(key) - (op != "photo_pyr_bwd"), 2)]
+        if op == "photo_pyr_bwd":
+            bases = [torch.randn(B, 8, h, w, device=device, generator=g) for h, w in hw]
+            coef = torch.rand(6 * len(hw), device=device, generator=g)
+            gl = torch.ones(2 * len(hw), device=device)
+            return lambda: ops.photo_loss_pyramid_backward(bases, coef, gl)
+        flows, i1, i2, m1, m2 = [], [], [], [], []
+        for h, w in hw:
+            yy = torch.linspace(0, 6.2832, h, device=device).view(1, 1, h, 1)
+            xx = torch.linspace(0, 6.2832, w, device=device).view(1, 1, 1, w)
+            ph = torch.rand(B, 2, 1, 1, device=device, generator=g) * 6.2832
+            f2 = torch.sin(2 * xx + ph) + torch.cos(3 * yy - ph)
+            flows.append(torch.cat([f2, -f2], 1).contiguous())
+            i1.append(torch.rand(B, C, h, w, device=device, generator=g))
+            i2.append(torch.rand(B, C, h, w, device=device, generator=g))
+            m1.append((torch.rand(B, 1, h, w, device=device, generator=g) > 0.1).float())
+            m2.append(m1[-1].flip(-1).contiguous())
+        return lambda: ops.photo_loss_pyramid_forward(flows, i1, i2, m1, m2, key[-1], need_grad=op == "photo_pyr_grad")
     if op == "occ_vis_pair":  # both directions of the loss's masks from a [B,4,H,W] flow
         B, _, H, W = key[:4]
         yy = torch.linspace(0, 6.2832, H, device=device).view(1, 1, H, 1)

@@ -457,6 +457,87 @@ def photo_loss_pair_forward(flow, im1, im2, mask1, mask2, pad: str = "border", w
     return out, basis
 
 
+def _host_array(ctype, values):
+    return (ctype * len(values))(*values)
+
+
+def photo_loss_pyramid_forward(flows, im1s, im2s, masks1, masks2, pad: str = "border", w_l1: float = 0.15,
+                               w_ssim: float = 0.85, need_grad: bool = False):
+    """:func:`photo_loss_pair_forward` for up to 4 loss scales in one launch
+    (usf_photo_loss_pyramid_fwd_f32; the largest scale first) -> (out
+    [nscale, 6] = {loss, c_l1, c_ssim} per direction per scale, bases: a list
+    of [B,8,H_k,W_k] or None)."""
+    import ctypes
+
+    if pad not in PAD_MODES:
+        raise NotImplementedError(f"flow_warp padding mode {pad!r} (supported: border, zeros)")
+    n = len(flows)
+    if not 1 <= n <= 4 or not (len(im1s) == len(im2s) == len(masks1) == len(masks2) == n):
+        raise ValueError(f"1..4 scales with one flow, two images and two masks each (got {n})")
+    args = []
+    for f, a, b_, m1, m2 in zip(flows, im1s, im2s, masks1, masks2):
+        a, b_, m1, B, C, H, W = _photo_args(a, b_, m1, None)
+        m2 = m2.contiguous()
+        _require_device_f32("mask2", m2)
+        _require_device_f32("flow", f)
+        if tuple(m2.shape) != (B, 1, H, W) or tuple(f.shape) != (B, 4, H, W):
+            raise ValueError(f"scale {len(args)}: mask2 {tuple(m2.shape)} / flow {tuple(f.shape)} vs {(B, C, H, W)}")
+        fv = f if f[0].is_contiguous() else f.contiguous()
+        args.append((fv, a, b_, m1, m2, B, C, H, W, fv.stride(0) if B > 1 else 4 * H * W))
+    B, C = args[0][5], args[0][6]
+    if any(x[5] != B or x[6] != C for x in args):
+        raise ValueError("every scale needs the same batch and channel count")
+    dev = args[0][1].device
+    Hs = _host_array(ctypes.c_int, [x[7] for x in args])
+    Ws = _host_array(ctypes.c_int, [x[8] for x in args])
+    lib = _lib.load()
+    npart = int(lib.usf_photo_loss_pyramid_partials(n, Hs, Ws, B))
+    partials = torch.empty(npart, device=dev, dtype=torch.float32)
+    out = torch.empty((n, 6), device=dev, dtype=torch.float32)
+    bases = [torch.empty((B, 8, x[7], x[8]), device=dev, dtype=torch.float32) for x in args] if need_grad else None
+    ptrs = lambda i: _host_array(ctypes.c_void_p, [x[i].data_ptr() for x in args])  # noqa: E731
+    nbytes = sum(4 * B * x[7] * x[8] * (2 * C + 4 + 2 + (8 if need_grad else 0)) for x in args)
+    op = "photo_pyr_grad" if need_grad else "photo_pyr"
+    key = (B, C) + tuple(v for x in args for v in (x[7], x[8])) + (pad,)
+    with torch.cuda.device(dev), _kt.timed(op, key, dev, nbytes):
+        rc = lib.usf_photo_loss_pyramid_fwd_f32(
+            n, ptrs(1), ptrs(2), ptrs(3), ptrs(4), ptrs(0), _host_array(ctypes.c_longlong, [x[9] for x in args]),
+            Hs, Ws, partials.data_ptr(), npart, out.data_ptr(),
+            _host_array(ctypes.c_void_p, [t.data_ptr() for t in bases]) if need_grad else None,
+            B, C, PAD_MODES[pad], float(w_l1), float(w_ssim), _lib.stream_handle(dev))
+    _lib.check(rc, "usf_photo_loss_pyramid_fwd_f32")
+    return out, bases
+
+
+def photo_loss_pyramid_backward(bases, coef, grad_losses):
+    """d(loss)/d(flow_k) * grad for every scale of :func:`photo_loss_pyramid_forward`
+    in one launch: bases [B,8,H_k,W_k], coef = its out [nscale, 6], grad_losses
+    [nscale, 2] -> list of [B,4,H_k,W_k] (deterministic)."""
+    import ctypes
+
+    n = len(bases)
+    for t in bases:
+        _require_device_f32("basis", t)
+    B = bases[0].shape[0]
+    dev = bases[0].device
+    gl = grad_losses.reshape(-1).to(torch.float32).contiguous()
+    if gl.numel() != 2 * n or coef.numel() != 6 * n:
+        raise ValueError(f"grad_losses / coef sizes {gl.numel()} / {coef.numel()} for {n} scales")
+    gflows = [torch.empty((B, 4) + tuple(t.shape[2:]), device=dev, dtype=torch.float32) for t in bases]
+    Hs = _host_array(ctypes.c_int, [t.shape[2] for t in bases])
+    Ws = _host_array(ctypes.c_int, [t.shape[3] for t in bases])
+    lib = _lib.load()
+    key = (B, 2) + tuple(v for t in bases for v in t.shape[2:])
+    nbytes = sum(4 * B * t.shape[2] * t.shape[3] * 12 for t in bases)
+    with torch.cuda.device(dev), _kt.timed("photo_pyr_bwd", key, dev, nbytes):
+        rc = lib.usf_photo_loss_pyramid_bwd_f32(
+            n, _host_array(ctypes.c_void_p, [t.contiguous().data_ptr() for t in bases]), coef.contiguous().data_ptr(),
+            gl.data_ptr(), _host_array(ctypes.c_void_p, [t.data_ptr() for t in gflows]), Hs, Ws, B,
+            _lib.stream_handle(dev))
+    _lib.check(rc, "usf_photo_loss_pyramid_bwd_f32")
+    return gflows
+
+
 def photo_loss_backward(basis, coef, grad_loss):
     """d(photo loss)/d(flow) * grad_loss from the forward's gradient basis
     ([B,4,H,W] one direction, [B,8,H,W] a pair) and coefficients ->

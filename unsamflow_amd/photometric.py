@@ -74,3 +74,43 @@ def photometric_loss_pair(flow: torch.Tensor, im1: torch.Tensor, im2: torch.Tens
         raise NotImplementedError("the fused photometric loss differentiates w.r.t. the flow only")
     return PhotometricPairFunction.apply(flow, im1, im2, mask1.detach(), mask2.detach(), pad, float(w_l1),
                                          float(w_ssim))
+
+
+class PhotometricPyramidFunction(Function):
+    """The with_bk pairs of up to 4 loss scales in one launch (the largest
+    first): returns [nscale, 2] losses; the gradient w.r.t. each scale's
+    [B,4,H,W] flow comes from one backward launch for all scales."""
+
+    @staticmethod
+    def forward(ctx, pad, w_l1, w_ssim, n, *tensors):
+        flows, im1s, im2s, m1s, m2s = (list(tensors[i * n:(i + 1) * n]) for i in range(5))
+        need = any(ctx.needs_input_grad[4:4 + n])
+        out, bases = ops.photo_loss_pyramid_forward(flows, im1s, im2s, m1s, m2s, pad, w_l1, w_ssim, need_grad=need)
+        ctx.n = n
+        if need:
+            ctx.save_for_backward(out, *bases)
+        return out[:, 0::3].clone()
+
+    @staticmethod
+    def backward(ctx, grad_losses):
+        n = ctx.n
+        grads = [None] * (4 + 5 * n)
+        if any(ctx.needs_input_grad[4:4 + n]):
+            out, *bases = ctx.saved_tensors
+            gflows = ops.photo_loss_pyramid_backward(bases, out, grad_losses)
+            for k in range(n):
+                if ctx.needs_input_grad[4 + k]:
+                    grads[4 + k] = gflows[k]
+        return tuple(grads)
+
+
+def photometric_loss_pyramid(flows, im1s, im2s, masks1, masks2, pad: str = "border", w_l1: float = 0.15,
+                             w_ssim: float = 0.85) -> torch.Tensor:
+    """``[photometric_loss_pair(flows[k], im1s[k], im2s[k], masks1[k], masks2[k]) for k]``
+    (flow_loss.py:120-148's scale loop, with_bk) as [nscale, 2] from ONE forward
+    launch and one backward launch; the same numbers as the per-scale calls."""
+    if any(t.requires_grad for t in list(im1s) + list(im2s)):
+        raise NotImplementedError("the fused photometric loss differentiates w.r.t. the flow only")
+    n = len(flows)
+    return PhotometricPyramidFunction.apply(pad, float(w_l1), float(w_ssim), n, *flows, *im1s, *im2s,
+                                            *[m.detach() for m in masks1], *[m.detach() for m in masks2])
