@@ -360,6 +360,29 @@ int usf_convex_upsample_bwd_f32(const float* flow, const float* mask, const floa
                                 float* grad_flow, float* grad_mask, float* scratch, int B, int H,
                                 int W, int factor, float mask_scale, void* stream);
 
+/* The decoder's output flows of every level (nlevel <= 6) through the convex
+ * x4 upsampler in ONE launch (factor 4 only): level l is
+ * usf_convex_upsample_f32(flow[l], mask[l], out[l], B, H[l], W[l], 4,
+ * mask_scale); the levels' blocks share one grid, the largest level first.
+ * Arrays are HOST arrays of device pointers. Results equal the per-level calls
+ * bit for bit. PWCLite defers the upsampling to the end of its decoder (the
+ * upsampled flows feed only the loss). */
+int usf_convex_upsample_pyramid_f32(int nlevel, const float* const* flow, const float* const* mask, float* const* out,
+                                    const int* H, const int* W, int B, int factor, float mask_scale, void* stream);
+
+/* Floats of scratch usf_convex_upsample_pyramid_bwd_f32 needs with grad_flow
+ * (the sum of usf_convex_upsample_bwd_scratch over the levels). */
+long long usf_convex_upsample_pyramid_bwd_scratch(int nlevel, const int* H, const int* W, int B);
+
+/* Its backward: usf_convex_upsample_bwd_f32 of every level in one launch (+
+ * one 9-tap gather launch for all grad_flows). grad_flow / grad_mask: NULL
+ * (not wanted) or host arrays of per-level device buffers. */
+int usf_convex_upsample_pyramid_bwd_f32(int nlevel, const float* const* flow, const float* const* mask,
+                                        const float* const* grad_out, float* const* grad_flow,
+                                        float* const* grad_mask, float* scratch, long long scratch_floats,
+                                        const int* H, const int* W, int B, int factor, float mask_scale,
+                                        void* stream);
+
 /* The loss's image pyramid (unFlowLoss per scale s: F.interpolate(im,
  * (H >> s, W >> s), mode="area"), flow_loss.py:128-129): out_s = mean of each
  * 2^s x 2^s block, summed in row-major order as torch's CPU kernel does

@@ -42,6 +42,8 @@ def test_header_declares_the_abi():
          "usf_photo_loss_pyramid_bwd_f32",
          "usf_flow_upsample_f32", "usf_flow_upsample_bwd_f32", "usf_area_pyramid_f32",
          "usf_convex_upsample_f32", "usf_convex_upsample_bwd_scratch", "usf_convex_upsample_bwd_f32",
+         "usf_convex_upsample_pyramid_f32", "usf_convex_upsample_pyramid_bwd_scratch",
+         "usf_convex_upsample_pyramid_bwd_f32",
          "usf_set_variant", "usf_device_errors", "usf_stream_copy_f32"]
     )
 

@@ -105,3 +105,30 @@ def test_upflow_network_fused_matches_torch_form(hip_device):
     torch.testing.assert_close(outs[1], outs[0], atol=1e-4, rtol=1e-5)
     for a, b in zip(grads[1], grads[0]):
         torch.testing.assert_close(a, b, atol=2e-3, rtol=1e-4)
+
+
+@pytest.mark.parametrize("B,sizes", [(16, [(64, 208), (32, 104), (16, 52), (8, 26), (4, 13)]),
+                                     (3, [(9, 7), (5, 4), (1, 1)])])
+def test_convex_pyramid_equals_per_level_calls(hip_device, B, sizes):
+    """convex_upsample_pyramid (usf_convex_upsample_pyramid_{f32,bwd_f32}:
+    every decoder level in one launch each way) gives the per-level
+    convex_upsample results bit for bit -- outputs, grad_flow and grad_mask --
+    at the decoder's batch-16 KITTI levels and odd sizes (incl. 1x1)."""
+    from unsamflow_amd.upsample import convex_upsample, convex_upsample_pyramid
+
+    gen = torch.Generator(device=hip_device).manual_seed(11)
+    flows = [torch.randn(B, 2, h, w, device=hip_device, generator=gen) for h, w in sizes]
+    masks = [torch.randn(B, 144, h, w, device=hip_device, generator=gen) for h, w in sizes]
+    gos = [torch.randn(B, 2, 4 * h, 4 * w, device=hip_device, generator=gen) for h, w in sizes]
+    fa = [f.clone().requires_grad_(True) for f in flows]
+    ma = [m.clone().requires_grad_(True) for m in masks]
+    fb = [f.clone().requires_grad_(True) for f in flows]
+    mb = [m.clone().requires_grad_(True) for m in masks]
+    ups = convex_upsample_pyramid(fa, ma, 4, 0.25)
+    refs = [convex_upsample(f, m, 4, 0.25) for f, m in zip(fb, mb)]
+    for u, r in zip(ups, refs):
+        assert torch.equal(u, r)
+    sum((u * g).sum() for u, g in zip(ups, gos)).backward()
+    sum((r * g).sum() for r, g in zip(refs, gos)).backward()
+    for a, b in zip(fa + ma, fb + mb):
+        assert torch.equal(a.grad, b.grad)

@@ -31,6 +31,9 @@ SITES += [("photo_fwd", (8, 3, 256 >> i, 832 >> i, "border")) for i in range(4)]
 SITES += [("photo_fwd_grad", (8, 3, 256 >> i, 832 >> i, "border")) for i in range(4)]
 SITES += [("photo_pair_grad", (8, 3, 256 >> i, 832 >> i, "border")) for i in range(4)]
 SITES += [("photo_bwd", (8, 2, 256 >> i, 832 >> i)) for i in range(4)]
+# every decoder level's convex upsampling in one launch (the training step's form; finest first)
+CPYR = tuple(v for _, H, W in KITTI[::-1] for v in (H, W))
+SITES += [("convex_pyr", (DB,) + CPYR + (4,)), ("convex_pyr_bwd", (DB,) + CPYR + (4,))]
 # the four loss scales in one launch (the training step's form)
 PYR = tuple(v for i in range(4) for v in (256 >> i, 832 >> i))
 SITES += [("photo_pyr_grad", (8, 3) + PYR + ("border",)), ("photo_pyr_bwd", (8, 2) + PYR)]

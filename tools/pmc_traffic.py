@@ -59,9 +59,9 @@ def launches(rows, nsites, n):
 
 
 def short(name):
-    """Kernel name without namespaces and argument lists."""
-    base = name.split("(")[0]
-    return base.replace("usf::(anonymous namespace)::", "").replace("usf::", "")
+    """Kernel name without return type, namespaces and argument list."""
+    n = name.replace("void ", "", 1).replace("usf::(anonymous namespace)::", "").replace("usf::", "")
+    return n.split("(")[0]
 
 
 def main():
@@ -94,7 +94,11 @@ def main():
                        "fetch_kib": round(statistics.median(launch[i][1] for launch in fl if len(launch) > i), 1),
                        "write_kib": round(statistics.median(launch[i][1] for launch in wl if len(launch) > i), 1)}
                       for i, nm in enumerate(names)]
-        if op in ("photo_pyr_grad", "photo_pyr_bwd"):
+        if op in ("convex_pyr", "convex_pyr_bwd"):
+            B, f = key[0], key[-1]
+            hw = [(key[i], key[i + 1]) for i in range(1, len(key) - 1, 2)]
+            H, W = hw[0]
+        elif op in ("photo_pyr_grad", "photo_pyr_bwd"):
             B, C = key[:2]
             hw = [(key[i], key[i + 1]) for i in range(2, len(key) - (op == "photo_pyr_grad"), 2)]
             H, W = hw[0]
@@ -131,6 +135,10 @@ def main():
             # both directions, every input read once: im1, im2, flow4,
             # both masks; the 8 basis planes written once (ops.photo_loss_pair_forward)
             alg = 4 * B * H * W * (2 * C + 4 + 2 + 8)
+        elif op == "convex_pyr":
+            alg = sum(4 * B * h * w * (2 + 11 * f * f) for h, w in hw)
+        elif op == "convex_pyr_bwd":
+            alg = sum(4 * B * h * w * (4 + 20 * f * f) for h, w in hw)
         elif op == "photo_pyr_grad":  # every scale's photo_pair_grad bytes
             alg = sum(4 * B * h * w * (2 * C + 4 + 2 + 8) for h, w in hw)
         elif op == "photo_pyr_bwd":  # basis in, grad_flow out, both directions per scale

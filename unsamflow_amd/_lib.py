@@ -132,6 +132,17 @@ _SIGNATURES = {
         [_c_float_p] * 6 + [ctypes.c_int] * 4 + [ctypes.c_float, ctypes.c_void_p],
         ctypes.c_int,
     ),
+    "usf_convex_upsample_pyramid_f32": (
+        [ctypes.c_int] + [ctypes.c_void_p] * 5 + [ctypes.c_int, ctypes.c_int, ctypes.c_float, ctypes.c_void_p],
+        ctypes.c_int,
+    ),
+    "usf_convex_upsample_pyramid_bwd_scratch": ([ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int],
+                                                ctypes.c_longlong),
+    "usf_convex_upsample_pyramid_bwd_f32": (
+        [ctypes.c_int] + [ctypes.c_void_p] * 5 + [_c_float_p, ctypes.c_longlong, ctypes.c_void_p, ctypes.c_void_p,
+                                                  ctypes.c_int, ctypes.c_int, ctypes.c_float, ctypes.c_void_p],
+        ctypes.c_int,
+    ),
     "usf_area_pyramid_f32": ([_c_float_p] * 4 + [ctypes.c_int] * 4 + [ctypes.c_void_p], ctypes.c_int),
     "usf_set_variant": ([ctypes.c_int, ctypes.c_int], ctypes.c_int),
     "usf_device_errors": ([ctypes.c_void_p, ctypes.c_int], ctypes.c_int),

@@ -685,6 +685,75 @@ int usf_convex_upsample_bwd_f32(const float* flow, const float* mask, const floa
                 (hipStream_t)stream);
 }
 
+static bool check_convex_pyr(const char* fn, int n, const int* H, const int* W, int B, int factor) {
+  if (n < 1 || n > convex_pyramid_max_levels() || !H || !W) {
+    set_error("%s: nlevel %d not in [1,%d] or null size arrays", fn, n, convex_pyramid_max_levels());
+    return false;
+  }
+  if (factor != 4) {
+    set_error("%s: factor %d (the pyramid form takes 4, the decoder's)", fn, factor);
+    return false;
+  }
+  for (int l = 0; l < n; ++l)
+    if (!check_convex(fn, B, H[l], W[l], factor)) return false;
+  return true;
+}
+
+long long usf_convex_upsample_pyramid_bwd_scratch(int nlevel, const int* H, const int* W, int B) {
+  if (nlevel < 1 || nlevel > convex_pyramid_max_levels() || !H || !W || B <= 0) return 0;
+  long long n = 0;
+  for (int l = 0; l < nlevel; ++l) n += convex_bwd_scratch(B, H[l], W[l]);
+  return n;
+}
+
+int usf_convex_upsample_pyramid_f32(int nlevel, const float* const* flow, const float* const* mask, float* const* out,
+                                    const int* H, const int* W, int B, int factor, float mask_scale, void* stream) {
+  clear_error();
+  const char* fn = "usf_convex_upsample_pyramid_f32";
+  if (!check_convex_pyr(fn, nlevel, H, W, B, factor)) return USF_EINVAL;
+  if (!flow || !mask || !out) {
+    set_error("%s: null pointer array", fn);
+    return USF_EINVAL;
+  }
+  for (int l = 0; l < nlevel; ++l)
+    if (!flow[l] || !mask[l] || !out[l]) {
+      set_error("%s: level %d: null pointer", fn, l);
+      return USF_EINVAL;
+    }
+  if (const int pe = pre_check(fn, (hipStream_t)stream)) return pe;
+  return finish(fn, convex_pyr_fwd_launch(nlevel, flow, mask, out, H, W, B, factor, mask_scale, (hipStream_t)stream),
+                (hipStream_t)stream);
+}
+
+int usf_convex_upsample_pyramid_bwd_f32(int nlevel, const float* const* flow, const float* const* mask,
+                                        const float* const* grad_out, float* const* grad_flow,
+                                        float* const* grad_mask, float* scratch, long long scratch_floats,
+                                        const int* H, const int* W, int B, int factor, float mask_scale,
+                                        void* stream) {
+  clear_error();
+  const char* fn = "usf_convex_upsample_pyramid_bwd_f32";
+  if (!check_convex_pyr(fn, nlevel, H, W, B, factor)) return USF_EINVAL;
+  if (!flow || !mask || !grad_out) {
+    set_error("%s: null input pointer array", fn);
+    return USF_EINVAL;
+  }
+  for (int l = 0; l < nlevel; ++l)
+    if (!flow[l] || !mask[l] || !grad_out[l] || (grad_flow && !grad_flow[l]) || (grad_mask && !grad_mask[l])) {
+      set_error("%s: level %d: null pointer", fn, l);
+      return USF_EINVAL;
+    }
+  if (grad_flow && (!scratch || scratch_floats < usf_convex_upsample_pyramid_bwd_scratch(nlevel, H, W, B))) {
+    set_error("%s: grad_flow needs scratch of usf_convex_upsample_pyramid_bwd_scratch floats", fn);
+    return USF_EINVAL;
+  }
+  if (!grad_flow && !grad_mask) return 0;
+  if (const int pe = pre_check(fn, (hipStream_t)stream)) return pe;
+  return finish(fn,
+                convex_pyr_bwd_launch(nlevel, flow, mask, grad_out, grad_flow, grad_mask, scratch, H, W, B, factor,
+                                      mask_scale, (hipStream_t)stream),
+                (hipStream_t)stream);
+}
+
 int usf_area_pyramid_f32(const float* x, float* out1, float* out2, float* out3, int B, int C, int H,
                          int W, void* stream) {
   clear_error();

@@ -109,16 +109,14 @@ __device__ __forceinline__ void load_run(const float* __restrict__ src, float (&
 }
 
 template <int S>
-__global__ __launch_bounds__(64 * S) void convex_up_fwd_kernel(const float* __restrict__ flow,
-                                                               const float* __restrict__ mask,
-                                                               float* __restrict__ out, int H, int W,
-                                                               float mask_scale) {
+__device__ __forceinline__ void convex_fwd_body(const float* __restrict__ flow, const float* __restrict__ mask,
+                                                float* __restrict__ out, int H, int W, float mask_scale, int blk,
+                                                int b) {
   constexpr int SS = S * S;
   const int lane = threadIdx.x & 63;
   const int i = threadIdx.x >> 6;  // sub-row of this wave
-  const int b = blockIdx.y;
   const int HW = H * W;
-  const int p = blockIdx.x * 64 + lane;
+  const int p = blk * 64 + lane;
   if (p >= HW) return;
   const int y = p / W, x = p - y * W;
   float v[2][9];
@@ -147,16 +145,24 @@ __global__ __launch_bounds__(64 * S) void convex_up_fwd_kernel(const float* __re
 }
 
 template <int S>
-__global__ __launch_bounds__(64 * S) void convex_up_bwd_kernel(
-    const float* __restrict__ flow, const float* __restrict__ mask, const float* __restrict__ gout,
-    float* __restrict__ gmask, float* __restrict__ gv, int H, int W, float mask_scale) {
+__global__ __launch_bounds__(64 * S) void convex_up_fwd_kernel(const float* __restrict__ flow,
+                                                               const float* __restrict__ mask,
+                                                               float* __restrict__ out, int H, int W,
+                                                               float mask_scale) {
+  convex_fwd_body<S>(flow, mask, out, H, W, mask_scale, blockIdx.x, blockIdx.y);
+}
+
+template <int S>
+__device__ __forceinline__ void convex_bwd_body(const float* __restrict__ flow, const float* __restrict__ mask,
+                                                const float* __restrict__ gout, float* __restrict__ gmask,
+                                                float* __restrict__ gv, int H, int W, float mask_scale, int blk,
+                                                int b) {
   constexpr int SS = S * S;
   __shared__ float red[S - 1][18][64];
   const int lane = threadIdx.x & 63;
   const int i = threadIdx.x >> 6;
-  const int b = blockIdx.y;
   const int HW = H * W;
-  const int p = blockIdx.x * 64 + lane;
+  const int p = blk * 64 + lane;
   const bool live = p < HW;  // no early return: the waves meet at a barrier
   const int pc = live ? p : HW - 1;
   const int y = pc / W, x = pc - y * W;
@@ -219,13 +225,18 @@ __global__ __launch_bounds__(64 * S) void convex_up_bwd_kernel(
   }
 }
 
+template <int S>
+__global__ __launch_bounds__(64 * S) void convex_up_bwd_kernel(
+    const float* __restrict__ flow, const float* __restrict__ mask, const float* __restrict__ gout,
+    float* __restrict__ gmask, float* __restrict__ gv, int H, int W, float mask_scale) {
+  convex_bwd_body<S>(flow, mask, gout, gmask, gv, H, W, mask_scale, blockIdx.x, blockIdx.y);
+}
+
 // grad_flow[b, c, q] = sum_k gv[b, c, k, q - offset_k]: unfold's backward (col2im)
 // as a fixed-order gather over the 9 taps.
-__global__ __launch_bounds__(256) void convex_up_gather_kernel(const float* __restrict__ gv,
-                                                               float* __restrict__ gflow, int B, int H,
-                                                               int W) {
+__device__ __forceinline__ void convex_gather_body(const float* __restrict__ gv, float* __restrict__ gflow, int B,
+                                                   int H, int W, long long t) {
   const int HW = H * W;
-  const long long t = (long long)blockIdx.x * 256 + threadIdx.x;
   if (t >= (long long)B * 2 * HW) return;
   const int q = (int)(t % HW);
   const int bc = (int)(t / HW);  // b * 2 + c
@@ -244,6 +255,57 @@ __global__ __launch_bounds__(256) void convex_up_gather_kernel(const float* __re
     }
   }
   gflow[t] = s;
+}
+
+__global__ __launch_bounds__(256) void convex_up_gather_kernel(const float* __restrict__ gv,
+                                                               float* __restrict__ gflow, int B, int H,
+                                                               int W) {
+  convex_gather_body(gv, gflow, B, H, W, (long long)blockIdx.x * 256 + threadIdx.x);
+}
+
+// The decoder's output flows of every level in ONE launch each way
+// (usf_convex_upsample_pyramid_{f32,bwd_f32}): level l owns blocks
+// [start[l], start[l + 1]) of the grid, the largest level first. The levels'
+// upsampled flows are independent of each other (only the loss reads them),
+// so PWCLite defers them to the end of the decoder.
+constexpr int kMaxLevels = 6;
+struct ConvexPyr {
+  const float* flow[kMaxLevels];
+  const float* mask[kMaxLevels];
+  const float* gout[kMaxLevels];
+  float* out[kMaxLevels];    // forward output / backward grad_flow
+  float* gmask[kMaxLevels];  // backward
+  float* gv[kMaxLevels];     // backward scratch of the level
+  int H[kMaxLevels], W[kMaxLevels];
+  int start[kMaxLevels + 1];
+  int n;
+};
+
+__device__ __forceinline__ int pyr_level(const ConvexPyr& m, int blk) {
+  int l = 0;
+#pragma unroll
+  for (int k = 1; k < kMaxLevels; ++k) l += blk >= m.start[k];
+  return l;
+}
+
+template <int S>
+__global__ __launch_bounds__(64 * S) void convex_pyr_fwd_kernel(ConvexPyr m, float mask_scale) {
+  const int l = pyr_level(m, blockIdx.x);
+  convex_fwd_body<S>(m.flow[l], m.mask[l], m.out[l], m.H[l], m.W[l], mask_scale, blockIdx.x - m.start[l],
+                     blockIdx.y);
+}
+
+template <int S>
+__global__ __launch_bounds__(64 * S) void convex_pyr_bwd_kernel(ConvexPyr m, float mask_scale) {
+  const int l = pyr_level(m, blockIdx.x);
+  convex_bwd_body<S>(m.flow[l], m.mask[l], m.gout[l], m.gmask[l], m.out[l] ? m.gv[l] : nullptr, m.H[l], m.W[l],
+                     mask_scale, blockIdx.x - m.start[l], blockIdx.y);
+}
+
+// start[] in 256-element blocks of each level's B * 2 * H * W outputs
+__global__ __launch_bounds__(256) void convex_pyr_gather_kernel(ConvexPyr m, int B) {
+  const int l = pyr_level(m, blockIdx.x);
+  convex_gather_body(m.gv[l], m.out[l], B, m.H[l], m.W[l], (long long)(blockIdx.x - m.start[l]) * 256 + threadIdx.x);
 }
 
 template <int S>
@@ -270,9 +332,83 @@ hipError_t convex_bwd_s(const float* flow, const float* mask, const float* gout,
   return hipGetLastError();
 }
 
+template <int S>
+hipError_t convex_pyr_fwd_s(ConvexPyr m, int B, float mask_scale, hipStream_t s) {
+  int total = 0;
+  for (int l = 0; l < m.n; ++l) {
+    m.start[l] = total;
+    total += (m.H[l] * m.W[l] + 63) / 64;
+  }
+  for (int l = m.n; l <= kMaxLevels; ++l) m.start[l] = total;
+  hipLaunchKernelGGL(convex_pyr_fwd_kernel<S>, dim3((unsigned)total, (unsigned)B), dim3(64 * S), 0, s, m,
+                     mask_scale);
+  return hipGetLastError();
+}
+
+template <int S>
+hipError_t convex_pyr_bwd_s(ConvexPyr m, int B, float mask_scale, bool want_flow, hipStream_t s) {
+  int total = 0;
+  for (int l = 0; l < m.n; ++l) {
+    m.start[l] = total;
+    total += (m.H[l] * m.W[l] + 63) / 64;
+  }
+  for (int l = m.n; l <= kMaxLevels; ++l) m.start[l] = total;
+  hipLaunchKernelGGL(convex_pyr_bwd_kernel<S>, dim3((unsigned)total, (unsigned)B), dim3(64 * S), 0, s, m,
+                     mask_scale);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess || !want_flow) return e;
+  total = 0;
+  for (int l = 0; l < m.n; ++l) {
+    m.start[l] = total;
+    total += (int)((2LL * B * m.H[l] * m.W[l] + 255) / 256);
+  }
+  for (int l = m.n; l <= kMaxLevels; ++l) m.start[l] = total;
+  hipLaunchKernelGGL(convex_pyr_gather_kernel, dim3((unsigned)total), dim3(256), 0, s, m, B);
+  return hipGetLastError();
+}
+
 }  // namespace
 
 bool convex_factor_ok(int factor) { return factor == 2 || factor == 4 || factor == 8; }
+
+int convex_pyramid_max_levels() { return kMaxLevels; }
+
+// largest level first (the launch order of the blocks)
+hipError_t convex_pyr_fwd_launch(int n, const float* const* flow, const float* const* mask, float* const* out,
+                                 const int* H, const int* W, int B, int factor, float mask_scale, hipStream_t s) {
+  if (n < 1 || n > kMaxLevels || factor != 4) return hipErrorInvalidValue;
+  ConvexPyr m{};
+  m.n = n;
+  for (int l = 0; l < n; ++l) {
+    m.flow[l] = flow[l];
+    m.mask[l] = mask[l];
+    m.out[l] = out[l];
+    m.H[l] = H[l];
+    m.W[l] = W[l];
+  }
+  return convex_pyr_fwd_s<4>(m, B, mask_scale, s);
+}
+
+hipError_t convex_pyr_bwd_launch(int n, const float* const* flow, const float* const* mask,
+                                 const float* const* gout, float* const* gflow, float* const* gmask, float* scratch,
+                                 const int* H, const int* W, int B, int factor, float mask_scale, hipStream_t s) {
+  if (n < 1 || n > kMaxLevels || factor != 4) return hipErrorInvalidValue;
+  ConvexPyr m{};
+  m.n = n;
+  long long off = 0;
+  for (int l = 0; l < n; ++l) {
+    m.flow[l] = flow[l];
+    m.mask[l] = mask[l];
+    m.gout[l] = gout[l];
+    m.out[l] = gflow ? gflow[l] : nullptr;
+    m.gmask[l] = gmask ? gmask[l] : nullptr;
+    m.gv[l] = gflow ? scratch + off : nullptr;
+    m.H[l] = H[l];
+    m.W[l] = W[l];
+    off += convex_bwd_scratch(B, H[l], W[l]);
+  }
+  return convex_pyr_bwd_s<4>(m, B, mask_scale, gflow != nullptr, s);
+}
 
 long long convex_bwd_scratch(int B, int H, int W) { return 18LL * B * H * W; }
 

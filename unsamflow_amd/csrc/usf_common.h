@@ -148,6 +148,12 @@ hipError_t upsample_fwd_launch(const float* x, float* out, int B, int C, int H, 
                                hipStream_t s);
 hipError_t upsample_bwd_launch(const float* gout, float* gx, int B, int C, int H, int W, int k,
                                hipStream_t s);
+int convex_pyramid_max_levels();
+hipError_t convex_pyr_fwd_launch(int n, const float* const* flow, const float* const* mask, float* const* out,
+                                 const int* H, const int* W, int B, int factor, float mask_scale, hipStream_t s);
+hipError_t convex_pyr_bwd_launch(int n, const float* const* flow, const float* const* mask,
+                                 const float* const* gout, float* const* gflow, float* const* gmask, float* scratch,
+                                 const int* H, const int* W, int B, int factor, float mask_scale, hipStream_t s);
 bool convex_factor_ok(int factor);
 long long convex_bwd_scratch(int B, int H, int W);
 hipError_t convex_fwd_launch(const float* flow, const float* mask, float* out, int B, int H, int W,

@@ -182,6 +182,15 @@ def site_launcher(op: str, key, device, seed: int = 0):
             return lambda: ops.flow_upsample(f, k)
         go = torch.randn(B, C, H * k, W * k, device=device, generator=g)
         return lambda: ops.flow_upsample_backward(go, k)
+    if op in ("convex_pyr", "convex_pyr_bwd"):  # every decoder level in one launch
+        B, f = key[0], key[-1]
+        hw = [(key[i], key[i + 1]) for i in range(1, len(key) - 1, 2)]
+        flows = [torch.randn(B, 2, h, w, device=device, generator=g) for h, w in hw]
+        masks = [torch.randn(B, 9 * f * f, h, w, device=device, generator=g) for h, w in hw]
+        if op == "convex_pyr":
+            return lambda: ops.convex_upsample_pyramid(flows, masks, f)
+        gos = [torch.randn(B, 2, f * h, f * w, device=device, generator=g) for h, w in hw]
+        return lambda: ops.convex_upsample_pyramid_backward(flows, masks, gos, f)
     if op in ("convex_up", "convex_up_bwd"):
         B, H, W, f = key
         flow = torch.randn(B, 2, H, W, device=device, generator=g)

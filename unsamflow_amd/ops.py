@@ -762,6 +762,73 @@ def convex_upsample_backward(flow: torch.Tensor, mask: torch.Tensor, grad_out: t
     return gf, gm
 
 
+def _level_sizes(flows):
+    import ctypes
+
+    return (_host_array(ctypes.c_int, [f.shape[2] for f in flows]),
+            _host_array(ctypes.c_int, [f.shape[3] for f in flows]))
+
+
+def convex_upsample_pyramid(flows, masks, factor: int = 4, mask_scale: float = 0.25):
+    """:func:`convex_upsample` of every decoder level in one launch
+    (usf_convex_upsample_pyramid_f32): flows [B,2,H_l,W_l], masks
+    [B,9f^2,H_l,W_l] -> list of [B,2,fH_l,fW_l]; the same numbers as the
+    per-level calls."""
+    import ctypes
+
+    n = len(flows)
+    fl = [f.contiguous() for f in flows]
+    mk = [m.contiguous() for m in masks]
+    for f, m in zip(fl, mk):
+        _require_device_f32("flow", f)
+        _require_device_f32("mask", m)
+    B, f_ = fl[0].shape[0], int(factor)
+    outs = [torch.empty((B, 2, f_ * f.shape[2], f_ * f.shape[3]), device=f.device, dtype=torch.float32) for f in fl]
+    Hs, Ws = _level_sizes(fl)
+    lib = _lib.load()
+    dev = fl[0].device
+    key = (B,) + tuple(v for f in fl for v in f.shape[2:]) + (f_,)
+    nbytes = sum(4 * B * f.shape[2] * f.shape[3] * (2 + 11 * f_ * f_) for f in fl)
+    ptrs = lambda ts: _host_array(ctypes.c_void_p, [t.data_ptr() for t in ts])  # noqa: E731
+    with torch.cuda.device(dev), _kt.timed("convex_pyr", key, dev, nbytes):
+        rc = lib.usf_convex_upsample_pyramid_f32(n, ptrs(fl), ptrs(mk), ptrs(outs), Hs, Ws, B, f_, float(mask_scale),
+                                                 _lib.stream_handle(dev))
+    _lib.check(rc, "usf_convex_upsample_pyramid_f32")
+    return outs
+
+
+def convex_upsample_pyramid_backward(flows, masks, grad_outs, factor: int = 4, mask_scale: float = 0.25,
+                                     need_flow: bool = True, need_mask: bool = True):
+    """(grad_flows, grad_masks) lists of :func:`convex_upsample_pyramid` (None where not needed)."""
+    import ctypes
+
+    n = len(flows)
+    fl = [f.contiguous() for f in flows]
+    mk = [m.contiguous() for m in masks]
+    go = [g.contiguous() for g in grad_outs]
+    B, f_ = fl[0].shape[0], int(factor)
+    if not (need_flow or need_mask):
+        return None, None
+    dev = fl[0].device
+    gfs = [torch.empty((B, 2) + tuple(f.shape[2:]), device=dev, dtype=torch.float32) for f in fl] if need_flow else None
+    gms = [torch.empty_like(m) for m in mk] if need_mask else None
+    Hs, Ws = _level_sizes(fl)
+    lib = _lib.load()
+    nscr = int(lib.usf_convex_upsample_pyramid_bwd_scratch(n, Hs, Ws, B)) if need_flow else 0
+    scratch = torch.empty(max(nscr, 1), device=dev, dtype=torch.float32)
+    ptrs = lambda ts: _host_array(ctypes.c_void_p, [t.data_ptr() for t in ts])  # noqa: E731
+    key = (B,) + tuple(v for f in fl for v in f.shape[2:]) + (f_,)
+    ff = f_ * f_
+    nbytes = sum(4 * B * f.shape[2] * f.shape[3] * (2 + 9 * ff + 2 * ff + (2 if need_flow else 0)
+                                                    + (9 * ff if need_mask else 0)) for f in fl)
+    with torch.cuda.device(dev), _kt.timed("convex_pyr_bwd", key, dev, nbytes):
+        rc = lib.usf_convex_upsample_pyramid_bwd_f32(n, ptrs(fl), ptrs(mk), ptrs(go), ptrs(gfs) if need_flow else None,
+                                                     ptrs(gms) if need_mask else None, scratch.data_ptr(), nscr, Hs,
+                                                     Ws, B, f_, float(mask_scale), _lib.stream_handle(dev))
+    _lib.check(rc, "usf_convex_upsample_pyramid_bwd_f32")
+    return gfs, gms
+
+
 def area_pyramid(x: torch.Tensor):
     """The loss's image pyramid: ``[F.interpolate(x, (H >> s, W >> s), mode="area")
     for s in 1, 2, 3]`` (flow_loss.py:128-129), one read of x, bit-exact with

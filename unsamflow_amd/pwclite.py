@@ -139,6 +139,10 @@ class UpFlowNetwork(nn.Module):
         up = torch.sum(weights * patches, dim=2)  # N,2,s,s,H,W
         return up.permute(0, 1, 4, 2, 5, 3).reshape(N, 2, s * H, s * W)
 
+    def mask(self, feat):
+        """The convs' raw upsampling mask (the 0.25 scale is applied by the op)."""
+        return self.convs(feat)
+
     def forward(self, flow, feat):
         if self.fused and flow.is_cuda:
             from .upsample import convex_upsample
@@ -226,7 +230,7 @@ class PWCLite(nn.Module):
         return F.interpolate(flow * k, scale_factor=k, mode="bilinear", align_corners=True)
 
     def decoder(self, x1_pyramid, x2_pyramid, full_seg1=None, full_seg2=None):
-        flows = []
+        flows, deferred = [], []
         B, _, h0, w0 = x1_pyramid[0].size()
         flow = torch.zeros(B, 2, h0, w0, dtype=x1_pyramid[0].dtype, device=x1_pyramid[0].device).float()
         for level, (x1, x2) in enumerate(zip(x1_pyramid, x2_pyramid)):
@@ -252,12 +256,21 @@ class PWCLite(nn.Module):
             flow = flow + flow_res
             flow_fine, up_feat = self.context_networks(torch.cat([x_intm, flow], dim=1))
             flow = flow + flow_fine
-            if self.output_flow_upsampler is not None:
-                flows.append(self.output_flow_upsampler(flow, up_feat))
+            up = self.output_flow_upsampler
+            if up is not None and up.fused and flow.is_cuda and up.scale == 4:
+                # the upsampled flows feed only the loss: every level's convex
+                # upsampling runs in one launch after the loop (the same numbers)
+                deferred.append((flow, up.mask(up_feat)))
+            elif up is not None:
+                flows.append(up(flow, up_feat))
             else:
                 flows.append(self._upsample(flow, 4))
             if level == self.output_level:
                 break
+        if deferred:  # finest level first: the largest level's blocks lead the grid
+            from .upsample import convex_upsample_pyramid
+
+            return convex_upsample_pyramid([f for f, _ in deferred[::-1]], [m for _, m in deferred[::-1]], 4, 0.25)
         return flows[::-1]
 
     @staticmethod

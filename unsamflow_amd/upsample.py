@@ -51,6 +51,36 @@ def convex_upsample(flow: torch.Tensor, mask: torch.Tensor, factor: int = 4, mas
     return ConvexUpsampleFunction.apply(flow, mask, int(factor), float(mask_scale))
 
 
+class ConvexUpsamplePyramidFunction(Function):
+    """Every decoder level's convex x4 upsampling in one launch each way."""
+
+    @staticmethod
+    def forward(ctx, factor, mask_scale, n, *tensors):
+        flows, masks = list(tensors[:n]), list(tensors[n:])
+        ctx.factor, ctx.mask_scale, ctx.n = factor, mask_scale, n
+        ctx.save_for_backward(*flows, *masks)
+        return tuple(ops.convex_upsample_pyramid(flows, masks, factor, mask_scale))
+
+    @staticmethod
+    def backward(ctx, *grad_outs):
+        n = ctx.n
+        saved = ctx.saved_tensors
+        flows, masks = list(saved[:n]), list(saved[n:])
+        need_f = any(ctx.needs_input_grad[3:3 + n])
+        need_m = any(ctx.needs_input_grad[3 + n:3 + 2 * n])
+        go = [g if g is not None else torch.zeros((f.shape[0], 2, ctx.factor * f.shape[2], ctx.factor * f.shape[3]),
+                                                  device=f.device) for g, f in zip(grad_outs, flows)]
+        gfs, gms = ops.convex_upsample_pyramid_backward(flows, masks, go, ctx.factor, ctx.mask_scale, need_f, need_m)
+        return (None, None, None, *(gfs if gfs is not None else [None] * n),
+                *(gms if gms is not None else [None] * n))
+
+
+def convex_upsample_pyramid(flows, masks, factor: int = 4, mask_scale: float = 0.25):
+    """``[convex_upsample(f, m, factor, mask_scale) for f, m in zip(flows, masks)]``
+    in one launch forward and one (+ one gather) backward."""
+    return list(ConvexUpsamplePyramidFunction.apply(int(factor), float(mask_scale), len(flows), *flows, *masks))
+
+
 def upsample_flow(flow: torch.Tensor, factor: int) -> torch.Tensor:
     """``F.interpolate(flow * factor, scale_factor=factor, mode="bilinear", align_corners=True)``."""
     return FlowUpsampleFunction.apply(flow, int(factor))
