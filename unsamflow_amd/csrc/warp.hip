@@ -546,6 +546,7 @@ __device__ __forceinline__ void cswap(int& a, int& b) {
 // (smooth flows: the tile shifted by the local flow, plus its spread), else
 // the sources are read from global memory directly.
 constexpr int kBoxW = 64, kBoxH = 16;  // staged box: rows of kBoxW floats (lane = column)
+
 constexpr int kBoxCap = kBoxW * kBoxH;
 template <bool PERSIST = false>
 __global__ __launch_bounds__(256) void warp_gx_bins_kernel(const float* __restrict__ gout, BinArgs ba,
@@ -659,34 +660,41 @@ __global__ __launch_bounds__(256) void warp_gx_bins_kernel(const float* __restri
       pk[k][j] = pk[k][j] < 0 ? 0 : staged ? (py - by0) * kBoxW + (px - bx0) : py * W + px;
     }
   // kGatherCH channels per pass with independent accumulators
+  // thread = (box row t / 16, column quad t % 16): kBoxH x kBoxW = 256 quads,
+  // so each thread stages at most one quad per channel, all loads in flight together
+  static_assert(kBoxH * kBoxW == 4 * 256, "one quad per thread and channel");
+  const int ry = t >> 4, rx = (t & 15) * 4;
+  const bool stager = staged && ry < bh && rx < bw;
+  const float* ssrc = gb + (size_t)(by0 + ry) * W + bx0 + rx;
+  auto stage_loads = [&](int c, float4 (&v)[kGatherCH]) {
+    if (w4) {
+#pragma unroll
+      for (int u = 0; u < kGatherCH; ++u)
+        v[u] = c + u < c1 ? *reinterpret_cast<const float4*>(ssrc + (size_t)(c + u) * HW)
+                          : make_float4(0.f, 0.f, 0.f, 0.f);
+    } else {  // unaligned rows: dword loads, none past the row
+      const int nv = min(4, W - (bx0 + rx));
+#pragma unroll
+      for (int u = 0; u < kGatherCH; ++u) {
+        const float* sc = ssrc + (size_t)min(c + u, c1 - 1) * HW;
+        const bool ok = c + u < c1;
+        v[u] = make_float4(ok ? sc[0] : 0.f, ok && nv > 1 ? sc[1] : 0.f, ok && nv > 2 ? sc[2] : 0.f,
+                           ok && nv > 3 ? sc[3] : 0.f);
+      }
+    }
+  };
+  // (Loading the next pass's quads into registers before this pass's sums --
+  // round 6 -- took the kernel from 116 to 144 VGPRs, 4 to 3 workgroups per CU:
+  // KITTI L4 in-step 64.9 vs 57.4 us, profiles/ab_r06/warp_gather_prefetch.json.)
   for (int c = c0; c < c1; c += kGatherCH) {
     float acc[kGatherCH];
 #pragma unroll
     for (int u = 0; u < kGatherCH; ++u) acc[u] = 0.f;
     if (staged) {
       __syncthreads();  // the previous pass is done with the box
-      // thread = (box row t / 16, column quad t % 16): kBoxH x kBoxW = 256 quads,
-      // so each thread stages at most one quad per channel, all loads in flight together
-      static_assert(kBoxH * kBoxW == 4 * 256, "one quad per thread and channel");
-      const int ry = t >> 4, rx = (t & 15) * 4;
-      if (ry < bh && rx < bw) {
-        const float* src = gb + (size_t)(by0 + ry) * W + bx0 + rx;
+      if (stager) {
         float4 v[kGatherCH];
-        if (w4) {
-#pragma unroll
-          for (int u = 0; u < kGatherCH; ++u)
-            v[u] = c + u < c1 ? *reinterpret_cast<const float4*>(src + (size_t)(c + u) * HW)
-                              : make_float4(0.f, 0.f, 0.f, 0.f);
-        } else {  // unaligned rows: dword loads, none past the row
-          const int nv = min(4, W - (bx0 + rx));
-#pragma unroll
-          for (int u = 0; u < kGatherCH; ++u) {
-            const float* sc = src + (size_t)min(c + u, c1 - 1) * HW;
-            const bool ok = c + u < c1;
-            v[u] = make_float4(ok ? sc[0] : 0.f, ok && nv > 1 ? sc[1] : 0.f, ok && nv > 2 ? sc[2] : 0.f,
-                               ok && nv > 3 ? sc[3] : 0.f);
-          }
-        }
+        stage_loads(c, v);
 #pragma unroll
         for (int u = 0; u < kGatherCH; ++u) *reinterpret_cast<float4*>(&box[u * kBoxCap + ry * kBoxW + rx]) = v[u];
       }
