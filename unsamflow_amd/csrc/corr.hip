@@ -1486,8 +1486,11 @@ constexpr int kBwdCandidates = 2;
 // -> 18.7, L1 18.7 -> 13.6 / 24.0 -> 17.2, L2 28.8 -> 25.4 / 32.9 -> 30.0,
 // config 1 18.7 -> 14.4, config 2 41.1 -> 40.4. From L3 up (512 units and more)
 // the ring's 60 KB cost a resident workgroup per CU: L3 38.9 -> 43.7, L4 74 -> 88.
+// SURVEY config 2 (exactly 256 units) is faster on the two-image tile with 4
+// channel groups: 39.0 / 43.6 vs 40.8 / 45.5 us warm / cold (round 6,
+// profiles/ab_r06/corr_variants.json), so the ring takes fewer than 256.
 #ifndef USF_BWD_RING_UNITS
-#define USF_BWD_RING_UNITS 256
+#define USF_BWD_RING_UNITS 192
 #endif
 
 template <int D>
