@@ -193,17 +193,19 @@ int usf_warp_bwd_ex_f32(const float* x, const float* flow, long long flow_bstrid
 /* Workspace bytes usf_warp_bwd_ex_f32 uses for the binned gather. */
 long long usf_warp_bwd_workspace(int B, int H, int W);
 
-/* usf_warp_bwd_ex_f32's binned gather in TWO launches (ABI 7): no per-call
- * zero fill and no overflow pass. workspace: usf_warp_bwd_persist_workspace
- * (B,C,H,W) bytes, 16-byte aligned, ZERO when first passed (one hipMemset at
- * allocation). It is then reserved for calls of this (B, C, H, W) on one
- * stream at a time; every call leaves it in a state the next call uses as is
- * (a parity word selects one of two cell-count buffers; the gather zeroes
- * the other), also under HIP graph replay. Pixels beyond 4 per cell are
- * scattered (fp32 atomics, summation order not fixed) into a dense overflow
- * buffer inside the workspace that the gather adds to its fixed-order sums
- * and re-zeroes. gx may be NULL (then no workspace is touched); C <= 256.
- * Results equal usf_warp_bwd_ex_f32's. */
+/* usf_warp_bwd_ex_f32's binned gather without the per-call zero fill (ABI 7):
+ * workspace: usf_warp_bwd_persist_workspace(B,C,H,W) bytes, 16-byte aligned,
+ * ZERO when first passed (one hipMemset at allocation). It is then reserved
+ * for calls of this (B, C, H, W), ordered on one stream at a time; every call
+ * leaves it in a state the next call uses as is (a parity word selects one of
+ * two cell-count buffers; the gather zeroes the other), also under HIP graph
+ * replay. Pixels beyond 4 per cell (fp32 atomics, summation order not fixed):
+ * up to H*W = 8192, TWO launches, those pixels scattered into a dense overflow
+ * buffer inside the workspace that the gather adds to its fixed-order sums and
+ * re-zeroes; above, THREE launches, the pixels listed (the list length under
+ * the same parity) and added by the overflow pass after the gather. gx may be
+ * NULL (then no workspace is touched); C <= 256. Results equal
+ * usf_warp_bwd_ex_f32's. */
 int usf_warp_bwd_persist_f32(const float* x, const float* flow, long long flow_bstride,
                              const float* gout, float* gx, float* gflow, void* workspace,
                              long long workspace_bytes, int B, int C, int H, int W, int pad_mode,

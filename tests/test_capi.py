@@ -190,11 +190,17 @@ def test_warp_bwd_workspace_size(lib):
 
 
 def test_warp_bwd_persist_workspace_size(lib):
-    """Persistent form: two count buffers, 4 slots + weights per cell, a dirty
-    word per gather tile, a dense [B,C,H,W] overflow buffer; 0 when invalid."""
-    B, C, H, W = 16, 32, 64, 208
+    """Persistent form: two count buffers, 4 slots + weights per cell, then up
+    to 8192 pixels a dirty word per gather tile and a dense [B,C,H,W] overflow
+    buffer, above that an overflow list of one int per pixel; 0 when invalid."""
+    B, C, H, W = 16, 32, 32, 104  # 3328 pixels: the dense overflow buffer
     n = lib.usf_warp_bwd_persist_workspace(B, C, H, W)
     cells = B * (H + 1) * (W + 1)
     lo = 4 * cells * (2 + 4 + 16) + 4 * B * C * H * W
-    assert lo <= n <= lo + 4 * B * 7 * 8 + 6 * 256
+    assert lo <= n <= lo + 4 * B * 4 * 4 + 6 * 256
+    B, C, H, W = 16, 32, 64, 208  # 13312 pixels: the list form
+    n = lib.usf_warp_bwd_persist_workspace(B, C, H, W)
+    cells = B * (H + 1) * (W + 1)
+    lo = 4 * cells * (2 + 4 + 16) + 4 * B * H * W
+    assert lo <= n <= lo + 5 * 256
     assert lib.usf_warp_bwd_persist_workspace(B, 0, H, W) == 0

@@ -1,6 +1,7 @@
-"""The two-launch persistent forms (ABI 7):
-usf_warp_bwd_persist_f32 (binned gather without the per-call zero fill and
-the overflow pass) and usf_occ_backward_persist_f32 (splat + threshold, the
+"""The persistent forms (ABI 7): usf_warp_bwd_persist_f32
+(binned gather without the per-call zero fill: two launches with a dense
+overflow buffer up to 8192 pixels, three -- the overflow pass kept -- in the
+list form above) and usf_occ_backward_persist_f32 (splat + threshold, the
 threshold re-zeroes the splat buffer). Their workspaces carry state from one
 call to the next, so every test runs a SEQUENCE of calls on one workspace --
 overflow-heavy, then smooth, then overflow-heavy again, and a second shape in
@@ -94,6 +95,38 @@ def test_warp_persist_workspace_returns_to_reusable_state(hip_device, monkeypatc
     cnt = ws[256:256 + 8 * cells].view(torch.int32).view(2, cells)
     nxt = int(hdr[0])
     assert nxt in (0, 1) and int(torch.count_nonzero(cnt[nxt])) == 0
+
+
+def test_warp_persist_list_form_returns_to_reusable_state(hip_device, monkeypatch):
+    """The list form (levels above USF_PERSIST_LIST_PIXELS = 8192 pixels: filing,
+    gather, overflow pass; no zero fill): after an overflow-heavy call and a
+    smooth one, the count buffer and the list length the parity selects for the
+    next call are zero, and every call matched the per-call form."""
+    monkeypatch.setattr(ops, "WARP_PERSIST_MAX_PIXELS", None)
+    B, C, H, W = 2, 8, 96, 100
+    g = torch.Generator(device=hip_device).manual_seed(37)
+    x = torch.randn(B, C, H, W, device=hip_device, generator=g)
+    go = torch.randn(B, C, H, W, device=hip_device, generator=g)
+    f = _fields(B, H, W, hip_device)
+    for kind in ("contract", "shift", "smooth", "contract", "smooth"):
+        gx, gf = ops.warp_backward(x, f[kind], go, "border")
+        rx, rf = _ex(x, f[kind], go, "border")
+        assert torch.equal(gf, rf), kind
+        if kind == "smooth":
+            assert torch.equal(gx, rx), kind
+        else:
+            torch.testing.assert_close(gx, rx, atol=1e-5, rtol=1e-5)
+    torch.cuda.synchronize()
+    ws = ops.persistent_workspace(hip_device, "warp_bwd", (B, C, H, W), 0)
+    # bin_layout2's list form, restated: header, 2 count buffers, slots, weights, overflow list
+    al = lambda v: (v + 255) & ~255  # noqa: E731
+    cells = B * (H + 1) * (W + 1)
+    ovf_off = al(al(al(256 + 8 * cells) + 16 * cells) + 64 * cells)
+    assert al(ovf_off + 4 * B * H * W) == int(_lib.load().usf_warp_bwd_persist_workspace(B, C, H, W))
+    hdr = ws[:16].view(torch.int32).cpu()
+    cnt = ws[256:256 + 8 * cells].view(torch.int32).view(2, cells)
+    nxt = int(hdr[0])
+    assert nxt in (0, 1) and int(torch.count_nonzero(cnt[nxt])) == 0 and int(hdr[2 + nxt]) == 0
 
 
 def test_occ_persist_call_sequence_matches_per_call_form(hip_device):

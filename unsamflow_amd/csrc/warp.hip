@@ -344,10 +344,12 @@ struct BinArgs {
   int* ovf = nullptr;      // [B * HW] overflow list: b * HW + p
   int* novf = nullptr;     // overflow list length
   int ovf_cap = 0;         // list capacity (B * HW): a pixel is listed at most once per call
-  // Persistent workspace (BIN == 2, usf_warp_bwd_persist_f32; see bwd_bins_persist):
-  // two count buffers chosen by a parity word, overflow pixels scattered into a
-  // dense [B][C][H][W] buffer that the gather adds and re-zeroes per dirty tile.
-  int* hdr = nullptr;          // [0]: parity the filing pass reads, [1]: the gather's
+  // Persistent workspace (BIN >= 2, usf_warp_bwd_persist_f32; see bwd_bins_persist):
+  // two count buffers chosen by a parity word; overflow pixels either scattered
+  // into a dense [B][C][H][W] buffer that the gather adds and re-zeroes per dirty
+  // tile (BIN == 2), or listed for the overflow pass with two list lengths chosen
+  // by the same parity (BIN == 3, the list form).
+  int* hdr = nullptr;          // [0]: parity the filing pass reads, [1]: the gather's, [2 + par]: list lengths
   int* cnt2 = nullptr;         // 2 x [B (H+1)(W+1)] count buffers
   float* ovfgx = nullptr;      // [B][C][H][W] overflow contributions (zero between calls)
   unsigned* dirty = nullptr;   // [B][tiles]: bit g = channel group g of the gather has overflow to add
@@ -365,9 +367,9 @@ __global__ __launch_bounds__(256) void warp_bwd_kernel(const float* __restrict__
                                                        int H, int W, BinArgs ba = {}) {
   constexpr int PXB = 256 / CS;
   __shared__ float red[2][256];
-  // BIN == 2: this call's count-buffer parity, loaded first so its latency
+  // BIN >= 2: this call's count-buffer parity, loaded first so its latency
   // overlaps the flow loads (the filing atomics need both)
-  const int par = BIN == 2 ? hdr_word(ba.hdr, 0) : 0;
+  const int par = BIN >= 2 ? hdr_word(ba.hdr, 0) : 0;
   const int HW = H * W;
   const int t = threadIdx.x;
   const int slice = t / PXB;
@@ -390,8 +392,8 @@ __global__ __launch_bounds__(256) void warp_bwd_kernel(const float* __restrict__
     // file p under its north-west corner cell (see BinArgs); weights as the scatter forms them
     if (tp.m_nw || tp.m_ne || tp.m_sw || tp.m_se) {  // then xw in [-1, W), yn in [-1, H)
       const size_t cell = (size_t)b * (H + 1) * (W + 1) + (size_t)(tp.yn + 1) * (W + 1) + (tp.xw + 1);
-      // BIN == 2: this call's count buffer, the one the parity selects
-      int* cnt = BIN == 2 ? ba.cnt2 + (size_t)at_use(par) * ba.ncell : ba.cnt;
+      // BIN >= 2: this call's count buffer, the one the parity selects
+      int* cnt = BIN >= 2 ? ba.cnt2 + (size_t)at_use(par) * ba.ncell : ba.cnt;
       const int slot = atomicAdd(cnt + cell, 1);
       if (slot < kBinSlots) {
         ba.bins[cell * kBinSlots + slot] = (p / W) << 16 | (p % W);  // (py, px): sorts as p
@@ -401,10 +403,11 @@ __global__ __launch_bounds__(256) void warp_bwd_kernel(const float* __restrict__
         wb[ks] = tp.m_ne ? tp.s * tp.w : 0.f;
         wb[2 * ks] = tp.m_sw ? tp.n * tp.e : 0.f;
         wb[3 * ks] = tp.m_se ? tp.n * tp.w : 0.f;
-      } else if (BIN == 1) {
+      } else if (BIN == 1 || BIN == 3) {
         // scattered by the overflow pass; the capacity test only matters if the
-        // per-call zero fill of novf / counts did not run (every pixel lists once)
-        const int o = atomicAdd(ba.novf, 1);
+        // per-call zero fill of novf / counts did not run (every pixel lists once).
+        // BIN == 3: the list length the parity selects (the gather zeroes the other)
+        const int o = atomicAdd(BIN == 3 ? ba.hdr + 2 + at_use(par) : ba.novf, 1);
         if (o < ba.ovf_cap) ba.ovf[o] = b * HW + p;
       } else {
         // persistent form: scattered below into ba.ovfgx; every gather workgroup of
@@ -421,7 +424,7 @@ __global__ __launch_bounds__(256) void warp_bwd_kernel(const float* __restrict__
   }
   // handed to the gather, which flips hdr[0] for the next call (one writer: a
   // same-address store from every workgroup would queue on one L2 line)
-  if (BIN == 2 && t == 0 && linear_block() == 0) ba.hdr[1] = at_use(par);
+  if (BIN >= 2 && t == 0 && linear_block() == 0) ba.hdr[1] = at_use(par);
   // grad_x: reduce-by-key over the wave per corner row (see scatter_row)
   RowRuns rn{}, rs{};
   if (WANT_GX) {
@@ -548,7 +551,9 @@ __device__ __forceinline__ void cswap(int& a, int& b) {
 constexpr int kBoxW = 64, kBoxH = 16;  // staged box: rows of kBoxW floats (lane = column)
 
 constexpr int kBoxCap = kBoxW * kBoxH;
-template <bool PERSIST = false>
+// PM: 0 per-call workspace, 1 persistent with the dense overflow buffer, 2
+// persistent list form (the overflow pass follows)
+template <int PM = 0>
 __global__ __launch_bounds__(256) void warp_gx_bins_kernel(const float* __restrict__ gout, BinArgs ba,
                                                            float* __restrict__ gx, int C, int H, int W,
                                                            int tiles_x, int cper) {
@@ -567,11 +572,12 @@ __global__ __launch_bounds__(256) void warp_gx_bins_kernel(const float* __restri
   // selects; both buffers' counts are loaded beside the parity (no dependent
   // load before the gather's own), and the other buffer is zeroed at the end
   // for the next call, which reads the flipped parity
+  constexpr bool PERSIST = PM > 0;
   const int par = PERSIST ? hdr_word(ba.hdr, 1) : 0;
   // both count buffers (2 x ncell ints < 2 GiB: capi.cpp bounds the shapes)
   const auto crs = __builtin_amdgcn_make_buffer_rsrc(PERSIST ? ba.cnt2 : ba.cnt, 0,
                                                      (int)(PERSIST ? 8 * ba.ncell : 4), 0x00020000);
-  const unsigned dword = PERSIST ? ba.dirty[(size_t)b * ba.ntiles + blockIdx.x] : 0u;
+  const unsigned dword = PM == 1 ? ba.dirty[(size_t)b * ba.ntiles + blockIdx.x] : 0u;
   if (t == 0) {
     bb[0] = INT_MAX; bb[1] = INT_MIN; bb[2] = INT_MAX; bb[3] = INT_MIN;
   }
@@ -721,7 +727,7 @@ __global__ __launch_bounds__(256) void warp_gx_bins_kernel(const float* __restri
             for (int u = 0; u < kGatherCH; ++u) acc[u] = fmaf(wk[k][j], src[co[u]], acc[u]);
           }
     }
-    const bool dirty = PERSIST && ((dword >> blockIdx.z) & 1u);  // overflow to add for this channel group
+    const bool dirty = PM == 1 && ((dword >> blockIdx.z) & 1u);  // overflow to add for this channel group
     if (dirty && valid) {
       // the overflow pixels' contributions (scattered by the filing pass), then
       // re-zeroed: this workgroup is their only reader
@@ -740,13 +746,17 @@ __global__ __launch_bounds__(256) void warp_gx_bins_kernel(const float* __restri
     }
   }
   if (PERSIST) {
-    if (((dword >> blockIdx.z) & 1u) && t == 0)
+    if (PM == 1 && ((dword >> blockIdx.z) & 1u) && t == 0)
       atomicAnd(ba.dirty + (size_t)b * ba.ntiles + blockIdx.x, ~(1u << blockIdx.z));
     const int pv = at_use(par);  // (a VGPR: no scalar copy of the parity is hoisted to its load)
     int* other = ba.cnt2 + (size_t)(1 - pv) * ba.ncell;
     const long long nth = (long long)gridDim.x * gridDim.y * gridDim.z * 256;
     for (long long i = (long long)linear_block() * 256 + t; i < ba.ncell; i += nth) other[i] = 0;
-    if (linear_block() == 0 && t == 0) ba.hdr[0] = 1 - pv;
+    if (linear_block() == 0 && t == 0) {
+      ba.hdr[0] = 1 - pv;
+      // list form: the next call's list length (this call's overflow pass reads hdr[2 + pv])
+      if (PM == 2) ba.hdr[2 + (1 - pv)] = 0;
+    }
   }
 }
 
@@ -773,7 +783,8 @@ __global__ __launch_bounds__(256) void warp_gx_ovf_kernel(const float* __restric
                                                           const float* __restrict__ gout, BinArgs ba,
                                                           float* __restrict__ gx, int C, int H, int W) {
   const int HW = H * W;
-  const int listed = *ba.novf;
+  // list form: the length this call's filing pass counted (parity hdr[1])
+  const int listed = ba.hdr ? ba.hdr[2 + (ba.hdr[1] & 1)] : *ba.novf;
   const int n = min(listed, ba.ovf_cap);
   const int lane = threadIdx.x & 63;
   if ((listed < 0 || listed > ba.ovf_cap) && blockIdx.x == 0 && threadIdx.x == 0)
@@ -1016,7 +1027,7 @@ void bwd_bins(const float* x, const float* flow, long long fbs, const float* gou
   (void)zero_fill(w, (size_t)(L.cnt_off + 4LL * B * (H + 1) * (W + 1)), s);  // novf + counts
   bin_pass<BORDER, 1>(x, flow, fbs, gout, gflow, B, C, H, W, ba, s);
   const GatherGrid gg = gather_grid(B, C, H, W);
-  hipLaunchKernelGGL(warp_gx_bins_kernel<false>, dim3((unsigned)gg.ntiles, (unsigned)B, (unsigned)gg.zg), dim3(256),
+  hipLaunchKernelGGL(warp_gx_bins_kernel<0>, dim3((unsigned)gg.ntiles, (unsigned)B, (unsigned)gg.zg), dim3(256),
                      0, s, gout, ba, gx, C, H, W, gg.tiles_x, gg.cper);
   // overflow pixels (few or none for smooth flows): listed, scattered with atomics
   hipLaunchKernelGGL((warp_gx_ovf_kernel<BORDER>), dim3(256), dim3(256), 0, s, flow, fbs, gout, ba, gx, C, H, W);
@@ -1034,21 +1045,44 @@ void bwd_bins(const float* x, const float* flow, long long fbs, const float* gou
 // each gather channel group; that group's workgroup adds the buffer into its
 // sums and zeroes it again (its only reader). The summation order of a cell
 // is the bins' (fixed), then the overflow sum, as in the four-launch form.
+//
+// List form (levels above USF_PERSIST_LIST_PIXELS pixels): THREE launches, the
+// overflow handled as in the four-launch form -- listed by the filing pass and
+// added by warp_gx_ovf_kernel after the gather -- with the list length kept
+// under the same parity as the counts (hdr[2 + par]; the gather zeroes the
+// other one), so no zero fill runs. At KITTI L4 (64 x 208) the dense buffer's
+// overflow path cost the filing pass and the gather ~7 us each for 48 overflow
+// pixels of the training step's own flow (tools/warp_flow_capture.py +
+// tools/warp_form_prof.py: 24.3 + 27.7 us vs 17.3 + 21.0 + 6.0 + 4.8 us for the
+// four-launch form), while the four-launch form paid its zero fill.
+#ifndef USF_PERSIST_LIST_PIXELS
+#define USF_PERSIST_LIST_PIXELS 8192
+#endif
+inline bool persist_list(int H, int W) { return (long long)H * W > USF_PERSIST_LIST_PIXELS; }
 struct BinLayout2 {
-  long long hdr_off, cnt_off, bins_off, wbin_off, dirty_off, ovfgx_off, total;
+  long long hdr_off, cnt_off, bins_off, wbin_off, dirty_off, ovfgx_off, ovf_off, total;
+  bool list;
 };
 inline BinLayout2 bin_layout2(int B, int C, int H, int W) {
   auto al = [](long long v) { return (v + 255) & ~255LL; };
   const long long E = (long long)B * (H + 1) * (W + 1);
   const GatherGrid gg = gather_grid(B, C, H, W);
   BinLayout2 L;
+  L.list = persist_list(H, W);
   L.hdr_off = 0;
   L.cnt_off = 256;
   L.bins_off = al(L.cnt_off + 2 * 4 * E);
   L.wbin_off = al(L.bins_off + 4 * E * kBinSlots);
-  L.dirty_off = al(L.wbin_off + 16 * E * kBinSlots);
-  L.ovfgx_off = al(L.dirty_off + 4LL * B * gg.ntiles);
-  L.total = al(L.ovfgx_off + 4LL * B * C * H * W);
+  if (L.list) {  // the overflow list (one entry per pixel at most)
+    L.dirty_off = L.ovfgx_off = -1;
+    L.ovf_off = al(L.wbin_off + 16 * E * kBinSlots);
+    L.total = al(L.ovf_off + 4LL * B * H * W);
+  } else {
+    L.ovf_off = -1;
+    L.dirty_off = al(L.wbin_off + 16 * E * kBinSlots);
+    L.ovfgx_off = al(L.dirty_off + 4LL * B * gg.ntiles);
+    L.total = al(L.ovfgx_off + 4LL * B * C * H * W);
+  }
   return L;
 }
 
@@ -1064,14 +1098,22 @@ void bwd_bins_persist(const float* x, const float* flow, long long fbs, const fl
   ba.bins = reinterpret_cast<int*>(w + L.bins_off);
   ba.wbin = reinterpret_cast<float*>(w + L.wbin_off);
   ba.ncell = (long long)B * (H + 1) * (W + 1);
+  ba.tiles_x = gg.tiles_x;
+  ba.ntiles = gg.ntiles;
+  const dim3 ggrid((unsigned)gg.ntiles, (unsigned)B, (unsigned)gg.zg);
+  if (L.list) {
+    ba.ovf = reinterpret_cast<int*>(w + L.ovf_off);
+    ba.ovf_cap = B * H * W;
+    bin_pass<BORDER, 3>(x, flow, fbs, gout, gflow, B, C, H, W, ba, s);
+    hipLaunchKernelGGL(warp_gx_bins_kernel<2>, ggrid, dim3(256), 0, s, gout, ba, gx, C, H, W, gg.tiles_x, gg.cper);
+    hipLaunchKernelGGL((warp_gx_ovf_kernel<BORDER>), dim3(256), dim3(256), 0, s, flow, fbs, gout, ba, gx, C, H, W);
+    return;
+  }
   ba.dirty = reinterpret_cast<unsigned*>(w + L.dirty_off);
   ba.ovfgx = reinterpret_cast<float*>(w + L.ovfgx_off);
   ba.dmask = gg.zg >= 32 ? ~0u : (1u << gg.zg) - 1u;
-  ba.tiles_x = gg.tiles_x;
-  ba.ntiles = gg.ntiles;
   bin_pass<BORDER, 2>(x, flow, fbs, gout, gflow, B, C, H, W, ba, s);
-  hipLaunchKernelGGL(warp_gx_bins_kernel<true>, dim3((unsigned)gg.ntiles, (unsigned)B, (unsigned)gg.zg), dim3(256),
-                     0, s, gout, ba, gx, C, H, W, gg.tiles_x, gg.cper);
+  hipLaunchKernelGGL(warp_gx_bins_kernel<1>, ggrid, dim3(256), 0, s, gout, ba, gx, C, H, W, gg.tiles_x, gg.cper);
 }
 
 // grad_x paths (usf_set_variant(2, v), benchmarking only): 0 = the lane-merged
@@ -1351,9 +1393,10 @@ __global__ __launch_bounds__(256) void zero_check_kernel(const unsigned* __restr
 }
 // the warp backward's next count buffer is the one the parity word selects
 __global__ __launch_bounds__(256) void cnt_check_kernel(const int* __restrict__ hdr, const unsigned* __restrict__ cnt2,
-                                                        long long ncell) {
+                                                        long long ncell, bool list) {
   const int par = hdr[0];
   bool bad = par != 0 && par != 1;
+  if (list && blockIdx.x == 0 && threadIdx.x == 0) bad |= hdr[2 + (par & 1)] != 0;  // the next list length
   const unsigned* c = cnt2 + (size_t)(par & 1) * ncell;
   for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < ncell; i += (long long)gridDim.x * 256)
     bad |= c[i] != 0u;
@@ -1376,8 +1419,9 @@ hipError_t warp_persist_check_launch(void* ws, int B, int C, int H, int W, hipSt
   const long long ncell = (long long)B * (H + 1) * (W + 1);
   hipLaunchKernelGGL(cnt_check_kernel, dim3((unsigned)std::min<long long>((ncell + 255) / 256, 2048)), dim3(256),
                      0, s, reinterpret_cast<const int*>(w + L.hdr_off),
-                     reinterpret_cast<const unsigned*>(w + L.cnt_off), ncell);
+                     reinterpret_cast<const unsigned*>(w + L.cnt_off), ncell, L.list);
   hipError_t e = hipGetLastError();
+  if (L.list) return e;
   if (e == hipSuccess) e = zero_check_launch(w + L.dirty_off, 4LL * B * gg.ntiles, s);
   if (e == hipSuccess) e = zero_check_launch(w + L.ovfgx_off, 4LL * B * C * H * W, s);
   return e;

@@ -225,12 +225,16 @@ def clear_persistent_workspaces() -> None:
     _PERSIST.clear()
 
 
-# The largest level (H*W pixels) that takes the persistent two-launch warp
-# backward; larger ones take the four-launch form (None: every level). Chosen by
-# the in-step time of the training step (tools/instep_ab.py, same process,
-# alternating, 4 rounds; profiles/ab_r06/warp_form_instep.json): KITTI L3
-# (32x104) 34.3 us persistent vs 38.7 four-launch, L4 (64x208) 65.2 vs 61.2.
-WARP_PERSIST_MAX_PIXELS: int | None = 8192
+# The largest level (H*W pixels) that takes the persistent warp backward
+# (usf_warp_bwd_persist_f32); larger ones take the four-launch per-call form
+# (None: every level). The library picks the persistent layout by size: up to
+# 8192 pixels two launches with a dense overflow buffer, above that three (the
+# overflow listed and added by the overflow pass; no zero fill). Chosen by the
+# in-step time of the training step (tools/instep_ab.py, same process,
+# alternating, 6 rounds; profiles/ab_r06/warp_form_list.json): KITTI L4 (64x208)
+# 55.4 us in the list form vs 59.0 four-launch; the dense form there was 68.8
+# (profiles/ab_r06/warp_form_instep_r2.json).
+WARP_PERSIST_MAX_PIXELS: int | None = None
 
 
 def warp_backward(
@@ -243,13 +247,15 @@ def warp_backward(
 ) -> tuple[torch.Tensor | None, torch.Tensor | None]:
     """(grad_x, grad_flow) of :func:`warp_forward`.
 
-    grad_x is the library's binned gather in its two-launch persistent form
-    (``usf_warp_bwd_persist_f32``): every source pixel is filed under its
+    grad_x is the library's binned gather in its persistent form
+    (``usf_warp_bwd_persist_f32``, two launches up to 8192 pixels, three above
+    with the overflow pass and no zero fill): every source pixel is filed under its
     north-west corner cell and each target cell sums its sources in a fixed
     order, so grad_x is deterministic unless a cell receives more than 4 source
     pixels (strongly compressive flow), whose excess is added with fp32
-    atomics. Its workspace (``usf_warp_bwd_persist_workspace``: ~88 B per pixel
-    plus one float per element of x) is kept per (device, shape) and ordered
+    atomics. Its workspace (``usf_warp_bwd_persist_workspace``: ~88 B per pixel,
+    plus one float per element of x up to 8192 pixels, one int per pixel above)
+    is kept per (device, shape) and ordered
     across streams (:func:`persistent_workspace`). grad_flow is deterministic."""
     _require_device_f32("x", x)
     _require_device_f32("flow12", flow)
@@ -267,7 +273,7 @@ def warp_backward(
     gx = torch.empty_like(xc) if need_x else None  # overwritten by the library
     gf = torch.empty((B, 2, H, W), device=x.device, dtype=torch.float32) if need_flow else None
     lib = _lib.load()
-    # grad_x by the binned gather, persistent two-launch form (C <= 256), else the
+    # grad_x by the binned gather, persistent form (C <= 256), else the
     # four-launch form with a per-call workspace from torch's caching allocator
     # (the C ABI's limits of the persistent form: a 32-bit dirty mask of channel
     # groups, packed (y, x), both count buffers under 32-bit byte offsets)
