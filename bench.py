@@ -98,9 +98,10 @@ def cfg_for(name):
 
 
 def kernel_report(summary, device, steps, replay=True):
-    """Per call site: in-step time (events around each launch in the timed
-    region), device time of graph-replayed launches, algorithmic GB/s and HBM
-    fraction; plus the roofline of the dominant site (by in-step time)."""
+    """Per call site: in-step time (events around each launch of an untimed pass
+    of the same step), device time of graph-replayed launches, algorithmic GB/s
+    and HBM fraction; plus the roofline of the dominant site (by in-step time),
+    whose mean main() then replaces by the timed region's own."""
     from unsamflow_amd.kernel_timer import device_time_cold_us, device_time_us, site_launcher, site_name
 
     rows, per_op = [], {}
@@ -494,15 +495,29 @@ def main():
         run = lambda: step(img1, img2, s1, s2)  # noqa: E731
     sync()
 
+    # eager: every hot-path launch's in-step time from an untimed pass of the same
+    # step (two event records around each launch cost ~0.3 ms of a 40 ms step,
+    # tools/kt_overhead.py); inside the timed region only the dominant call site
+    # (the roofline kernel) carries its events. Graph replays carry no host code,
+    # so their per-site times come from the eager pass after the timed region.
+    site_pass = None
+    roof_site = None
+    if on_gpu and not use_graph:
+        with KernelTimer() as site_pass:
+            for _ in range(max(3, min(args.steps, 10))):
+                run()
+            sync()
+        per_site = site_pass.summary()
+        if per_site:
+            n_pass = max(3, min(args.steps, 10))
+            roof_site = max(per_site.items(), key=lambda kv: kv[1]["n"] / n_pass * kv[1]["mean_us"])[0]
     if distributed:
         dist.barrier()
     sync()
-    # eager: two event records per hot-path launch inside the timed region (no syncs);
-    # graph replays carry no host code, so their per-site times come from the
-    # in-step pass below
     if on_gpu and not use_graph:
         step.phase_events = []  # (start, after backward, end) device events per timed step
-    with KernelTimer(enabled=on_gpu and not use_graph) as kt:
+    with KernelTimer(enabled=on_gpu and not use_graph and roof_site is not None,
+                     only={roof_site}) as kt:
         t0 = time.perf_counter()
         for _ in range(args.steps):
             loss = run()
@@ -538,8 +553,21 @@ def main():
 
     rows = roof = per_op_us = gpu_configs = None
     if on_gpu:
-        summary = kt.summary()
-        rows, roof, per_op_us = kernel_report(summary, device, args.steps, replay=not args.no_replay)
+        if site_pass is not None:
+            # per-site rows from the untimed pass; the roofline site's mean from
+            # the timed region itself (its launches only were bracketed there)
+            n_pass = max(3, min(args.steps, 10))
+            rows, roof, per_op_us = kernel_report(site_pass.summary(), device, n_pass, replay=not args.no_replay)
+            timed_site = kt.summary().get(roof_site)
+            if timed_site and (roof["kernel"], tuple(roof["shape"])) == roof_site:
+                us = timed_site["mean_us"]
+                roof["site_pass_mean_us"] = roof["mean_us"]
+                roof["mean_us"] = round(us, 2)
+                roof["achieved"] = round(roof["bytes_per_launch"] / (us * 1e-6) / 1e9, 1)
+                roof["frac"] = round(roof["bytes_per_launch"] / (us * 1e-6) / 1e9 / HBM_PEAK_GBPS, 4)
+                roof["launches_timed"] = timed_site["n"]
+        else:
+            rows, roof, per_op_us = kernel_report(kt.summary(), device, args.steps, replay=not args.no_replay)
         roof["copy_ceiling_gbps"] = copy_ceiling_gbps(device)
         roof["frac_of_copy"] = round(roof["achieved"] / roof["copy_ceiling_gbps"], 4)
         traffic, src, note = pmc_traffic(roof["kernel"], roof["shape"])

@@ -79,9 +79,12 @@ def warp_bytes(B, C, H, W, backward=False, need_x=True, need_flow=True):
 
 
 class KernelTimer:
-    def __init__(self, time_in_step: bool = True, enabled: bool = True):
+    def __init__(self, time_in_step: bool = True, enabled: bool = True, only=None):
         self.time_in_step = time_in_step
         self.enabled = enabled  # False: a no-op context (nothing recorded)
+        # only: a set of (op, key) call sites to bracket (None: every launch), so a
+        # timed region can carry the events of one site and no others
+        self.only = only
         self.records = []  # (op, key, start_event, end_event, bytes, flops)
 
     def __enter__(self):
@@ -117,7 +120,7 @@ def timed(op: str, key, device, nbytes: int, flops: int = 0):
         rx.roctxRangePushA(site_name(op, key).encode())
     try:
         kt = _active
-        if kt is None:
+        if kt is None or (kt.only is not None and (op, tuple(key)) not in kt.only):
             yield
             return
         if not kt.time_in_step:
