@@ -65,15 +65,14 @@ def corr_forward(x1: torch.Tensor, x2: torch.Tensor, max_displacement: int,
         _check_out("output", out, (B, K * K, H, W), x1.device)
     lib = _lib.load()
     ws, nws = _corr_workspace(lib, B, C, H, W, d, x1.device)
+    _args = (x1c.data_ptr(), x2c.data_ptr(), out.data_ptr(), K * K * H * W, 0, 0.0, None,
+             ws.data_ptr() if nws else None, nws, B, C, H, W, d, _lib.stream_handle(x1.device),)
     with torch.cuda.device(x1.device), _kt.timed(
         "corr_fwd", (B, C, H, W), x1.device, _kt.corr_bytes(B, C, H, W, K * K), _kt.corr_flops(B, C, H, W, K * K)
     ):
         # the _ex entry with a dense output stride: same result as usf_corr_fwd_f32,
         # plus the channel-split workspace for the small levels
-        rc = lib.usf_corr_fwd_ex_f32(
-            x1c.data_ptr(), x2c.data_ptr(), out.data_ptr(), K * K * H * W, 0, 0.0, None,
-            ws.data_ptr() if nws else None, nws, B, C, H, W, d, _lib.stream_handle(x1.device)
-        )
+        rc = lib.usf_corr_fwd_ex_f32(*_args)
     _lib.check(rc, "usf_corr_fwd_ex_f32")
     return out
 
@@ -119,15 +118,14 @@ def corr_backward(
         g2 = torch.empty_like(x2c) if gx2_out is None else gx2_out
         _check_out("grad_input2", g2, (B, C, H, W), x1.device)
     lib = _lib.load()
+    _args = (x1c.data_ptr(), x2c.data_ptr(), gc.data_ptr(), _ptr(g1), _ptr(g2), B, C, H, W, d,
+             _lib.stream_handle(x1.device),)
     with torch.cuda.device(x1.device), _kt.timed(
         "corr_bwd", (B, C, H, W, need_x1, need_x2), x1.device,
         _kt.corr_bytes(B, C, H, W, K * K, True, need_x1, need_x2),
         _kt.corr_flops(B, C, H, W, K * K, True, need_x1, need_x2),
     ):
-        rc = lib.usf_corr_bwd_f32(
-            x1c.data_ptr(), x2c.data_ptr(), gc.data_ptr(), _ptr(g1), _ptr(g2),
-            B, C, H, W, d, _lib.stream_handle(x1.device),
-        )
+        rc = lib.usf_corr_bwd_f32(*_args)
     _lib.check(rc, "usf_corr_bwd_f32")
     return g1, g2
 
@@ -160,11 +158,10 @@ def warp_forward(x: torch.Tensor, flow: torch.Tensor, pad: str = "border") -> to
     fv, fbs = _flow_view(flow, B, H, W)
     out = torch.empty_like(xc)
     lib = _lib.load()
+    _args = (xc.data_ptr(), fv.data_ptr(), fbs, out.data_ptr(), B, C, H, W, PAD_MODES[pad],
+             _lib.stream_handle(x.device),)
     with torch.cuda.device(x.device), _kt.timed("warp_fwd", (B, C, H, W, pad), x.device, _kt.warp_bytes(B, C, H, W)):
-        rc = lib.usf_warp_fwd_f32(
-            xc.data_ptr(), fv.data_ptr(), fbs, out.data_ptr(), B, C, H, W, PAD_MODES[pad],
-            _lib.stream_handle(x.device),
-        )
+        rc = lib.usf_warp_fwd_f32(*_args)
     _lib.check(rc, "usf_warp_fwd_f32")
     return out
 
@@ -288,10 +285,11 @@ def warp_backward(
             nws = int(lib.usf_warp_bwd_workspace(B, H, W)) if need_x else 0
             ws = torch.empty(nws, device=x.device, dtype=torch.uint8) if nws > 0 else None
         fn = lib.usf_warp_bwd_persist_f32 if persist else lib.usf_warp_bwd_ex_f32
+        _args = (xc.data_ptr(), fv.data_ptr(), fbs, gc.data_ptr(), _ptr(gx), _ptr(gf), _ptr(ws), nws, B, C, H, W,
+                 PAD_MODES[pad], _lib.stream_handle(x.device),)
         with _kt.timed("warp_bwd", (B, C, H, W, pad, need_x, need_flow), x.device,
                        _kt.warp_bytes(B, C, H, W, True, need_x, need_flow)):
-            rc = fn(xc.data_ptr(), fv.data_ptr(), fbs, gc.data_ptr(), _ptr(gx), _ptr(gf), _ptr(ws), nws,
-                    B, C, H, W, PAD_MODES[pad], _lib.stream_handle(x.device))
+            rc = fn(*_args)
     if rc != 0 and persist:
         _drop_workspace(x.device, "warp_bwd", (B, C, H, W))
     _lib.check(rc, "usf_warp_bwd_persist_f32" if persist else "usf_warp_bwd_ex_f32")
@@ -315,10 +313,10 @@ def splat_map(flow: torch.Tensor, absolute: bool = False) -> torch.Tensor:
     fv, fbs, B, H, W = _flow_arg(flow, "flow")
     out = torch.empty((B, 1, H, W), device=flow.device, dtype=torch.float32)
     lib = _lib.load()
+    _args = (fv.data_ptr(), fbs, out.data_ptr(), B, H, W, int(bool(absolute)), _lib.stream_handle(flow.device),)
     with torch.cuda.device(flow.device), _kt.timed("splat", (B, 1, H, W, bool(absolute)), flow.device,
                                                      4 * B * H * W * 3):
-        rc = lib.usf_splat_map_f32(fv.data_ptr(), fbs, out.data_ptr(), B, H, W, int(bool(absolute)),
-                                   _lib.stream_handle(flow.device))
+        rc = lib.usf_splat_map_f32(*_args)
     _lib.check(rc, "usf_splat_map_f32")
     return out
 
@@ -333,9 +331,10 @@ def occ_backward(flow21: torch.Tensor, th: float = 0.2) -> torch.Tensor:
         # re-zeroes (usf_occ_backward_persist_f32: two launches, no fill)
         nmap = 4 * B * H * W
         ws = persistent_workspace(flow21.device, "occ_bwd", (B, H, W), nmap)
+        _args = (fv.data_ptr(), fbs, out.data_ptr(), ws.data_ptr(), nmap, B, H, W, float(th),
+                 _lib.stream_handle(flow21.device),)
         with _kt.timed("occ_bwd", (B, 1, H, W), flow21.device, 4 * B * H * W * 3):
-            rc = lib.usf_occ_backward_persist_f32(fv.data_ptr(), fbs, out.data_ptr(), ws.data_ptr(), nmap, B, H, W,
-                                                  float(th), _lib.stream_handle(flow21.device))
+            rc = lib.usf_occ_backward_persist_f32(*_args)
     if rc != 0:
         _drop_workspace(flow21.device, "occ_bwd", (B, H, W))
     _lib.check(rc, "usf_occ_backward_persist_f32")
@@ -359,9 +358,10 @@ def occ_vis_pair(flow4: torch.Tensor, th: float = 0.2) -> torch.Tensor:
     with torch.cuda.device(f.device):
         nmap = 8 * B * H * W
         ws = persistent_workspace(f.device, "occ_vis_pair", (B, H, W), nmap)
+        _args = (f.data_ptr(), 4 * H * W, vis.data_ptr(), ws.data_ptr(), nmap, B, H, W, float(th),
+                 _lib.stream_handle(f.device),)
         with _kt.timed("occ_vis_pair", (B, 1, H, W), f.device, 4 * B * H * W * 6):
-            rc = lib.usf_occ_vis_pair_persist_f32(f.data_ptr(), 4 * H * W, vis.data_ptr(), ws.data_ptr(), nmap, B, H,
-                                                  W, float(th), _lib.stream_handle(f.device))
+            rc = lib.usf_occ_vis_pair_persist_f32(*_args)
     if rc != 0:
         _drop_workspace(f.device, "occ_vis_pair", (B, H, W))
     _lib.check(rc, "usf_occ_vis_pair_persist_f32")
@@ -377,10 +377,11 @@ def occ_bidirection(flow12: torch.Tensor, flow21: torch.Tensor, scale: float = 0
         raise ValueError(f"flow21 shape {tuple(flow21.shape)} != flow12 shape {tuple(flow12.shape)}")
     out = torch.empty((B, 1, H, W), device=flow12.device, dtype=torch.float32)
     lib = _lib.load()
+    _args = (f1.data_ptr(), bs1, f2.data_ptr(), bs2, out.data_ptr(), B, H, W, float(scale), float(bias),
+             _lib.stream_handle(flow12.device),)
     with torch.cuda.device(flow12.device), _kt.timed("occ_bidir", (B, 1, H, W), flow12.device,
                                                        4 * B * H * W * 5):
-        rc = lib.usf_occ_bidirection_f32(f1.data_ptr(), bs1, f2.data_ptr(), bs2, out.data_ptr(), B, H, W,
-                                         float(scale), float(bias), _lib.stream_handle(flow12.device))
+        rc = lib.usf_occ_bidirection_f32(*_args)
     _lib.check(rc, "usf_occ_bidirection_f32")
     return out
 
@@ -417,12 +418,11 @@ def photo_loss_forward(src, tgt, mask, flow, pad: str = "border", w_l1: float = 
     # algorithmic bytes: src, tgt, mask, flow read once; the basis written once
     nbytes = 4 * B * H * W * (2 * C + 3 + (4 if need_grad else 0))
     op = "photo_fwd_grad" if need_grad else "photo_fwd"
+    _args = (s.data_ptr(), t.data_ptr(), m.data_ptr(), fv.data_ptr(), fbs, partials.data_ptr(), out.data_ptr(),
+             basis.data_ptr() if need_grad else None, B, C, H, W, PAD_MODES[pad], float(w_l1), float(w_ssim),
+             _lib.stream_handle(src.device),)
     with torch.cuda.device(src.device), _kt.timed(op, (B, C, H, W, pad), src.device, nbytes):
-        rc = lib.usf_photo_loss_fwd_f32(s.data_ptr(), t.data_ptr(), m.data_ptr(), fv.data_ptr(), fbs,
-                                        partials.data_ptr(), out.data_ptr(),
-                                        basis.data_ptr() if need_grad else None, B, C, H, W,
-                                        PAD_MODES[pad], float(w_l1), float(w_ssim),
-                                        _lib.stream_handle(src.device))
+        rc = lib.usf_photo_loss_fwd_f32(*_args)
     _lib.check(rc, "usf_photo_loss_fwd_f32")
     return out, basis
 
@@ -453,12 +453,11 @@ def photo_loss_pair_forward(flow, im1, im2, mask1, mask2, pad: str = "border", w
     # 4-channel flow, both masks; with the gradient the 8 basis planes written once
     nbytes = 4 * B * H * W * (2 * C + 4 + 2 + (8 if need_grad else 0))
     op = "photo_pair_grad" if need_grad else "photo_pair"
+    _args = (a.data_ptr(), b_.data_ptr(), m1.data_ptr(), m2.data_ptr(), fv.data_ptr(), fbs, partials.data_ptr(),
+             out.data_ptr(), basis.data_ptr() if need_grad else None, B, C, H, W, PAD_MODES[pad], float(w_l1),
+             float(w_ssim), _lib.stream_handle(im1.device),)
     with torch.cuda.device(im1.device), _kt.timed(op, (B, C, H, W, pad), im1.device, nbytes):
-        rc = lib.usf_photo_loss_pair_fwd_f32(a.data_ptr(), b_.data_ptr(), m1.data_ptr(), m2.data_ptr(),
-                                             fv.data_ptr(), fbs, partials.data_ptr(), out.data_ptr(),
-                                             basis.data_ptr() if need_grad else None, B, C, H, W,
-                                             PAD_MODES[pad], float(w_l1), float(w_ssim),
-                                             _lib.stream_handle(im1.device))
+        rc = lib.usf_photo_loss_pair_fwd_f32(*_args)
     _lib.check(rc, "usf_photo_loss_pair_fwd_f32")
     return out, basis
 
@@ -505,12 +504,12 @@ def photo_loss_pyramid_forward(flows, im1s, im2s, masks1, masks2, pad: str = "bo
     nbytes = sum(4 * B * x[7] * x[8] * (2 * C + 4 + 2 + (8 if need_grad else 0)) for x in args)
     op = "photo_pyr_grad" if need_grad else "photo_pyr"
     key = (B, C) + tuple(v for x in args for v in (x[7], x[8])) + (pad,)
+    _args = (n, ptrs(1), ptrs(2), ptrs(3), ptrs(4), ptrs(0), _host_array(ctypes.c_longlong, [x[9] for x in args]),
+             Hs, Ws, partials.data_ptr(), npart, out.data_ptr(),
+             _host_array(ctypes.c_void_p, [t.data_ptr() for t in bases]) if need_grad else None, B, C,
+             PAD_MODES[pad], float(w_l1), float(w_ssim), _lib.stream_handle(dev),)
     with torch.cuda.device(dev), _kt.timed(op, key, dev, nbytes):
-        rc = lib.usf_photo_loss_pyramid_fwd_f32(
-            n, ptrs(1), ptrs(2), ptrs(3), ptrs(4), ptrs(0), _host_array(ctypes.c_longlong, [x[9] for x in args]),
-            Hs, Ws, partials.data_ptr(), npart, out.data_ptr(),
-            _host_array(ctypes.c_void_p, [t.data_ptr() for t in bases]) if need_grad else None,
-            B, C, PAD_MODES[pad], float(w_l1), float(w_ssim), _lib.stream_handle(dev))
+        rc = lib.usf_photo_loss_pyramid_fwd_f32(*_args)
     _lib.check(rc, "usf_photo_loss_pyramid_fwd_f32")
     return out, bases
 
@@ -535,11 +534,11 @@ def photo_loss_pyramid_backward(bases, coef, grad_losses):
     lib = _lib.load()
     key = (B, 2) + tuple(v for t in bases for v in t.shape[2:])
     nbytes = sum(4 * B * t.shape[2] * t.shape[3] * 12 for t in bases)
+    _args = (n, _host_array(ctypes.c_void_p, [t.contiguous().data_ptr() for t in bases]),
+             coef.contiguous().data_ptr(), gl.data_ptr(),
+             _host_array(ctypes.c_void_p, [t.data_ptr() for t in gflows]), Hs, Ws, B, _lib.stream_handle(dev),)
     with torch.cuda.device(dev), _kt.timed("photo_pyr_bwd", key, dev, nbytes):
-        rc = lib.usf_photo_loss_pyramid_bwd_f32(
-            n, _host_array(ctypes.c_void_p, [t.contiguous().data_ptr() for t in bases]), coef.contiguous().data_ptr(),
-            gl.data_ptr(), _host_array(ctypes.c_void_p, [t.data_ptr() for t in gflows]), Hs, Ws, B,
-            _lib.stream_handle(dev))
+        rc = lib.usf_photo_loss_pyramid_bwd_f32(*_args)
     _lib.check(rc, "usf_photo_loss_pyramid_bwd_f32")
     return gflows
 
@@ -559,10 +558,11 @@ def photo_loss_backward(basis, coef, grad_loss):
         raise ValueError(f"grad_loss has {gl.numel()} elements for {ndir} direction(s)")
     gflow = torch.empty((B, 2 * ndir, H, W), device=basis.device, dtype=torch.float32)
     lib = _lib.load()
+    _args = (basis.data_ptr(), coef.data_ptr(), gl.data_ptr(), gflow.data_ptr(), B, H, W, ndir,
+             _lib.stream_handle(basis.device),)
     with torch.cuda.device(basis.device), _kt.timed("photo_bwd", (B, ndir, H, W), basis.device,
                                                       4 * B * H * W * 6 * ndir):
-        rc = lib.usf_photo_loss_bwd_f32(basis.data_ptr(), coef.data_ptr(), gl.data_ptr(), gflow.data_ptr(),
-                                        B, H, W, ndir, _lib.stream_handle(basis.device))
+        rc = lib.usf_photo_loss_bwd_f32(*_args)
     _lib.check(rc, "usf_photo_loss_bwd_f32")
     return gflow
 
@@ -620,12 +620,12 @@ def corr_forward_ex(x1: torch.Tensor, x2: torch.Tensor, max_displacement: int, o
     # is its own timing site, so its device time is measured on the same call
     op = "corr_fwd_leaky" if act else "corr_fwd"
     nbytes = _kt.corr_bytes(B, C, H, W, K * K) + (8 * act_mask.numel() if act_mask is not None else 0)
+    _args = (x1c.data_ptr(), x2c.data_ptr(), out.data_ptr(), obs, act, float(leaky_slope or 0.0), _ptr(act_mask),
+             ws.data_ptr() if nws else None, nws, B, C, H, W, d, _lib.stream_handle(x1.device),)
     with torch.cuda.device(x1.device), _kt.timed(
         op, (B, C, H, W), x1.device, nbytes, _kt.corr_flops(B, C, H, W, K * K)
     ):
-        rc = lib.usf_corr_fwd_ex_f32(x1c.data_ptr(), x2c.data_ptr(), out.data_ptr(), obs, act,
-                                     float(leaky_slope or 0.0), _ptr(act_mask), ws.data_ptr() if nws else None, nws,
-                                     B, C, H, W, d, _lib.stream_handle(x1.device))
+        rc = lib.usf_corr_fwd_ex_f32(*_args)
     _lib.check(rc, "usf_corr_fwd_ex_f32")
     return out
 
@@ -674,13 +674,13 @@ def corr_backward_ex(x1: torch.Tensor, x2: torch.Tensor, grad_out: torch.Tensor,
         nbytes += 4 * B * H * W * K * K
     elif act_mask is not None:
         nbytes += 8 * act_mask.numel()
+    _args = (x1c.data_ptr(), x2c.data_ptr(), grad_out.data_ptr(), gbs, _ptr(act_out), _ptr(act_mask),
+             float(leaky_slope), _ptr(scratch), _ptr(g1), _ptr(g2), B, C, H, W, d, _lib.stream_handle(x1.device),)
     with torch.cuda.device(x1.device), _kt.timed(
         op, (B, C, H, W, need_x1, need_x2), x1.device, nbytes,
         _kt.corr_flops(B, C, H, W, K * K, True, need_x1, need_x2),
     ):
-        rc = lib.usf_corr_bwd_ex_f32(x1c.data_ptr(), x2c.data_ptr(), grad_out.data_ptr(), gbs, _ptr(act_out),
-                                     _ptr(act_mask), float(leaky_slope), _ptr(scratch), _ptr(g1), _ptr(g2), B, C, H, W, d,
-                                     _lib.stream_handle(x1.device))
+        rc = lib.usf_corr_bwd_ex_f32(*_args)
     _lib.check(rc, "usf_corr_bwd_ex_f32")
     return g1, g2
 
@@ -693,10 +693,10 @@ def flow_upsample(flow: torch.Tensor, factor: int) -> torch.Tensor:
     fc = flow.contiguous()
     out = torch.empty((B, C, H * k, W * k), device=flow.device, dtype=torch.float32)
     lib = _lib.load()
+    _args = (fc.data_ptr(), out.data_ptr(), B, C, H, W, k, _lib.stream_handle(flow.device),)
     with torch.cuda.device(flow.device), _kt.timed("upsample", (B, C, H, W, k), flow.device,
                                                      4 * B * C * H * W * (1 + k * k)):
-        rc = lib.usf_flow_upsample_f32(fc.data_ptr(), out.data_ptr(), B, C, H, W, k,
-                                       _lib.stream_handle(flow.device))
+        rc = lib.usf_flow_upsample_f32(*_args)
     _lib.check(rc, "usf_flow_upsample_f32")
     return out
 
@@ -711,10 +711,10 @@ def flow_upsample_backward(grad_out: torch.Tensor, factor: int) -> torch.Tensor:
     gc = grad_out.contiguous()
     gx = torch.empty((B, C, H, W), device=grad_out.device, dtype=torch.float32)
     lib = _lib.load()
+    _args = (gc.data_ptr(), gx.data_ptr(), B, C, H, W, k, _lib.stream_handle(grad_out.device),)
     with torch.cuda.device(grad_out.device), _kt.timed("upsample_bwd", (B, C, H, W, k), grad_out.device,
                                                          4 * B * C * H * W * (1 + k * k)):
-        rc = lib.usf_flow_upsample_bwd_f32(gc.data_ptr(), gx.data_ptr(), B, C, H, W, k,
-                                           _lib.stream_handle(grad_out.device))
+        rc = lib.usf_flow_upsample_bwd_f32(*_args)
     _lib.check(rc, "usf_flow_upsample_bwd_f32")
     return gx
 
@@ -734,9 +734,10 @@ def convex_upsample(flow: torch.Tensor, mask: torch.Tensor, factor: int = 4,
     out = torch.empty((B, 2, f * H, f * W), device=flow.device, dtype=torch.float32)
     lib = _lib.load()
     nbytes = 4 * B * H * W * (2 + 11 * f * f)
+    _args = (fc.data_ptr(), mc.data_ptr(), out.data_ptr(), B, H, W, f, float(mask_scale),
+             _lib.stream_handle(flow.device),)
     with torch.cuda.device(flow.device), _kt.timed("convex_up", (B, H, W, f), flow.device, nbytes):
-        rc = lib.usf_convex_upsample_f32(fc.data_ptr(), mc.data_ptr(), out.data_ptr(), B, H, W, f,
-                                         float(mask_scale), _lib.stream_handle(flow.device))
+        rc = lib.usf_convex_upsample_f32(*_args)
     _lib.check(rc, "usf_convex_upsample_f32")
     return out
 
@@ -760,10 +761,10 @@ def convex_upsample_backward(flow: torch.Tensor, mask: torch.Tensor, grad_out: t
         scratch = torch.empty(int(lib.usf_convex_upsample_bwd_scratch(B, H, W)), device=flow.device,
                               dtype=torch.float32)
     nbytes = 4 * B * H * W * (2 + 9 * f * f + 2 * f * f + (2 if need_flow else 0) + (9 * f * f if need_mask else 0))
+    _args = (fc.data_ptr(), mc.data_ptr(), gc.data_ptr(), _ptr(gf), _ptr(gm), _ptr(scratch), B, H, W, f,
+             float(mask_scale), _lib.stream_handle(flow.device),)
     with torch.cuda.device(flow.device), _kt.timed("convex_up_bwd", (B, H, W, f), flow.device, nbytes):
-        rc = lib.usf_convex_upsample_bwd_f32(fc.data_ptr(), mc.data_ptr(), gc.data_ptr(), _ptr(gf), _ptr(gm),
-                                             _ptr(scratch), B, H, W, f, float(mask_scale),
-                                             _lib.stream_handle(flow.device))
+        rc = lib.usf_convex_upsample_bwd_f32(*_args)
     _lib.check(rc, "usf_convex_upsample_bwd_f32")
     return gf, gm
 
@@ -796,9 +797,9 @@ def convex_upsample_pyramid(flows, masks, factor: int = 4, mask_scale: float = 0
     key = (B,) + tuple(v for f in fl for v in f.shape[2:]) + (f_,)
     nbytes = sum(4 * B * f.shape[2] * f.shape[3] * (2 + 11 * f_ * f_) for f in fl)
     ptrs = lambda ts: _host_array(ctypes.c_void_p, [t.data_ptr() for t in ts])  # noqa: E731
+    _args = (n, ptrs(fl), ptrs(mk), ptrs(outs), Hs, Ws, B, f_, float(mask_scale), _lib.stream_handle(dev),)
     with torch.cuda.device(dev), _kt.timed("convex_pyr", key, dev, nbytes):
-        rc = lib.usf_convex_upsample_pyramid_f32(n, ptrs(fl), ptrs(mk), ptrs(outs), Hs, Ws, B, f_, float(mask_scale),
-                                                 _lib.stream_handle(dev))
+        rc = lib.usf_convex_upsample_pyramid_f32(*_args)
     _lib.check(rc, "usf_convex_upsample_pyramid_f32")
     return outs
 
@@ -827,10 +828,10 @@ def convex_upsample_pyramid_backward(flows, masks, grad_outs, factor: int = 4, m
     ff = f_ * f_
     nbytes = sum(4 * B * f.shape[2] * f.shape[3] * (2 + 9 * ff + 2 * ff + (2 if need_flow else 0)
                                                     + (9 * ff if need_mask else 0)) for f in fl)
+    _args = (n, ptrs(fl), ptrs(mk), ptrs(go), ptrs(gfs) if need_flow else None, ptrs(gms) if need_mask else None,
+             scratch.data_ptr(), nscr, Hs, Ws, B, f_, float(mask_scale), _lib.stream_handle(dev),)
     with torch.cuda.device(dev), _kt.timed("convex_pyr_bwd", key, dev, nbytes):
-        rc = lib.usf_convex_upsample_pyramid_bwd_f32(n, ptrs(fl), ptrs(mk), ptrs(go), ptrs(gfs) if need_flow else None,
-                                                     ptrs(gms) if need_mask else None, scratch.data_ptr(), nscr, Hs,
-                                                     Ws, B, f_, float(mask_scale), _lib.stream_handle(dev))
+        rc = lib.usf_convex_upsample_pyramid_bwd_f32(*_args)
     _lib.check(rc, "usf_convex_upsample_pyramid_bwd_f32")
     return gfs, gms
 
@@ -847,8 +848,9 @@ def area_pyramid(x: torch.Tensor):
     outs = [torch.empty((B, C, H >> s, W >> s), device=x.device, dtype=torch.float32) for s in (1, 2, 3)]
     lib = _lib.load()
     nbytes = 4 * B * C * H * W * (1 + 1 / 4 + 1 / 16 + 1 / 64)
+    _args = (xc.data_ptr(), outs[0].data_ptr(), outs[1].data_ptr(), outs[2].data_ptr(), B, C, H, W,
+             _lib.stream_handle(x.device),)
     with torch.cuda.device(x.device), _kt.timed("area_pyramid", (B, C, H, W), x.device, int(nbytes)):
-        rc = lib.usf_area_pyramid_f32(xc.data_ptr(), outs[0].data_ptr(), outs[1].data_ptr(), outs[2].data_ptr(),
-                                      B, C, H, W, _lib.stream_handle(x.device))
+        rc = lib.usf_area_pyramid_f32(*_args)
     _lib.check(rc, "usf_area_pyramid_f32")
     return outs
