@@ -607,6 +607,8 @@ def main():
                 "parallelism": f"dp{world}",
             },
             "final_loss": round(loss_val, 6),
+            # untimed steps whose every hot-path launch was bracketed (the levels rows)
+            "site_pass_steps": 0 if site_pass is None else max(3, min(args.steps, 10)),
             # the step split as BASELINE.md 4 defines the metric: fwd + loss + bwd, and
             # the optimizer step (clip + Adam + scheduler) apart. ms_per_step and value
             # stay the all-in wall time of the timed region (the driver's clock)

@@ -6,7 +6,7 @@ and that run's kernel_stats.csv, where every hot-path launch is listed under
 its call-site name (unsamflow_amd.kernel_timer.site_name). Prints, for the
 roofline site and every other hot-path site, the bench's in-step event mean
 next to rocprof's summed kernel duration per launch of that site (rocprof
-also counts the warm-up steps; a site whose launch runs two kernels -- the
+also counts the warm-up steps and the untimed per-site pass; a site whose launch runs two kernels -- the
 split forward's reduce, the leaky backward's derivative pass, the photometric
 final reduction -- is the sum of both).
 
@@ -27,7 +27,11 @@ def main():
     bench = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
     stats = {r["Name"]: r for r in csv.DictReader(open(sys.argv[2]))}
     roof = bench["roofline"]
-    steps = bench["steps"] + bench["warmup"]
+    # every launch rocprof saw: warm-up, bench.py's untimed per-site pass, timed steps
+    site_pass = bench.get("site_pass_steps")
+    if site_pass is None:  # lines written before the field existed
+        site_pass = max(3, min(bench["steps"], 10)) if "site_pass_mean_us" in bench["roofline"] else 0
+    steps = bench["steps"] + bench["warmup"] + site_pass
     sites = []
     levels = bench["levels"]
     if levels and isinstance(levels[0], list):  # compact rows (bench.py LEVEL_FIELDS)
