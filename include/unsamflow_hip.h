@@ -18,6 +18,8 @@
  *   usf_warp_fwd_f32  <- grid_sample(bilinear, align_corners=True) inside
  *                        flow_warp (utils/warp_utils.py:97-106, incl.
  *                        mesh_grid :7-13 and norm_grid :16-23)
+ *   usf_warp_fwd_up_f32 <- the decoder's F.interpolate(flow * 2) followed by
+ *                        flow_warp (pwclite.py:299-302) in one launch
  *   usf_warp_bwd_f32 / usf_warp_bwd_ex_f32 / usf_warp_bwd_persist_f32
  *                     <- grid_sampler_2d_backward reached from flow_warp's
  *                        autograd graph (warp_utils.py:103-105)
@@ -166,6 +168,15 @@ long long usf_corr_bwd_ex_scratch(int B, int C, int H, int W, int d);
 int usf_warp_fwd_f32(const float* x, const float* flow, long long flow_bstride,
                      float* out, int B, int C, int H, int W, int pad_mode,
                      void* stream);
+
+/* The decoder's flow upsampling and warp in ONE launch (ABI 8; pwclite.py:299-302:
+ * flow = F.interpolate(coarse * 2, scale_factor=2, mode="bilinear",
+ * align_corners=True); x2_warp = flow_warp(x2, flow)). coarse_flow: dense
+ * [B,2,H/2,W/2] (H, W even); up_flow: dense [B,2,H,W], written (the same numbers
+ * as usf_flow_upsample_f32 with factor 2); out: [B,C,H,W] = usf_warp_fwd_f32(x,
+ * up_flow). */
+int usf_warp_fwd_up_f32(const float* x, const float* coarse_flow, float* up_flow, float* out, int B, int C, int H,
+                        int W, int pad_mode, void* stream);
 
 /* Backward of usf_warp_fwd_f32. gout: [B,C,H,W] dense.
  * gx: [B,C,H,W] or NULL; overwritten (the library zeroes it, then scatters

@@ -33,7 +33,7 @@ def test_header_declares_the_abi():
         ["usf_abi_version", "usf_build_id", "usf_last_error_string", "usf_corr_fwd_f32", "usf_corr_bwd_f32",
          "usf_corr_fwd_ex_f32", "usf_corr_fwd_workspace", "usf_corr_bwd_ex_f32", "usf_corr_act_mask_words",
          "usf_corr_bwd_ex_scratch",
-         "usf_warp_fwd_f32", "usf_warp_bwd_f32", "usf_warp_bwd_ex_f32", "usf_warp_bwd_workspace",
+         "usf_warp_fwd_f32", "usf_warp_fwd_up_f32", "usf_warp_bwd_f32", "usf_warp_bwd_ex_f32", "usf_warp_bwd_workspace",
          "usf_warp_bwd_persist_f32", "usf_warp_bwd_persist_workspace",
          "usf_splat_map_f32", "usf_occ_backward_f32", "usf_occ_backward_persist_f32", "usf_occ_vis_pair_persist_f32",
          "usf_occ_bidirection_f32",
@@ -94,6 +94,8 @@ def test_no_torch_types_in_abi():
         (lambda L: L.usf_corr_bwd_f32(1, 1, 1, 1, 1, 1, 4, 4, 4, 0, None), "max_displacement 0"),
         (lambda L: L.usf_warp_fwd_f32(1, 1, 32, 1, 1, 3, 4, 4, 7, None), "pad_mode 7"),
         (lambda L: L.usf_warp_fwd_f32(1, 1, 3, 1, 2, 3, 4, 4, 1, None), "batch stride"),
+        (lambda L: L.usf_warp_fwd_up_f32(1, 1, 1, 1, 2, 3, 5, 4, 1, None), "must be even"),
+        (lambda L: L.usf_warp_fwd_up_f32(1, None, 1, 1, 2, 3, 4, 4, 1, None), "null pointer"),
         (lambda L: L.usf_warp_bwd_f32(1, None, 32, 1, 1, 1, 1, 3, 4, 4, 1, None), "null input"),
         (lambda L: L.usf_warp_bwd_f32(1, 1, 32, 1, 1, 1, 1, 3, -4, 4, 1, None), "non-positive"),
         (lambda L: L.usf_warp_bwd_ex_f32(1, 1, 32, 1, 1, 1, 1, -5, 1, 3, 4, 4, 1, None), "negative workspace"),

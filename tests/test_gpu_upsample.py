@@ -132,3 +132,38 @@ def test_convex_pyramid_equals_per_level_calls(hip_device, B, sizes):
     sum((r * g).sum() for r, g in zip(refs, gos)).backward()
     for a, b in zip(fa + ma, fb + mb):
         assert torch.equal(a.grad, b.grad)
+
+
+@pytest.mark.parametrize("pad", ["border", "zeros"])
+@pytest.mark.parametrize("B,C,H,W", [(16, 128, 8, 26), (16, 32, 64, 208), (3, 5, 14, 32)])
+def test_upsample_warp_equals_separate_calls(hip_device, B, C, H, W, pad):
+    """usf_warp_fwd_up_f32 (the decoder's x2 upsampling + flow_warp of x2 in one
+    launch, pwclite.py:299-302) gives the same numbers as usf_flow_upsample_f32
+    followed by usf_warp_fwd_f32, bit for bit; its autograd form gives the
+    gradients of the two-op form (to the rounding of the binned gather's
+    overflow atomics and of the gradient sum order)."""
+    from unsamflow_amd import ops
+    from unsamflow_amd.upsample import upsample_flow, upsample_warp
+    from unsamflow_amd.warp_utils import flow_warp
+
+    coarse = torch.from_numpy(hashrng.symmetric((B, 2, H // 2, W // 2), 430 + C, 3.0)).to(hip_device)
+    x = torch.from_numpy(hashrng.normal((B, C, H, W), 431 + C)).to(hip_device)
+    g_up = torch.from_numpy(hashrng.normal((B, 2, H, W), 432 + C)).to(hip_device)
+    g_out = torch.from_numpy(hashrng.normal((B, C, H, W), 433 + C)).to(hip_device)
+    up_ref = ops.flow_upsample(coarse, 2)
+    out_ref = ops.warp_forward(x, up_ref, pad)
+    up, out = ops.warp_forward_up(x, coarse, pad)
+    assert torch.equal(up, up_ref) and torch.equal(out, out_ref)
+
+    c1, x1 = coarse.clone().requires_grad_(True), x.clone().requires_grad_(True)
+    u1 = upsample_flow(c1, 2)
+    o1 = flow_warp(x1, u1, pad)
+    torch.autograd.backward([u1, o1], [g_up, g_out])
+    c2, x2 = coarse.clone().requires_grad_(True), x.clone().requires_grad_(True)
+    u2, o2 = upsample_warp(c2, x2, pad)
+    assert torch.equal(u2, u1) and torch.equal(o2, o1)
+    torch.autograd.backward([u2, o2], [g_up, g_out])
+    # grad_x: cells with more than 4 sources (this random +-6 px field has them)
+    # add their excess with fp32 atomics, so two calls agree to rounding only
+    torch.testing.assert_close(x2.grad, x1.grad, atol=1e-5, rtol=1e-5)
+    torch.testing.assert_close(c2.grad, c1.grad, atol=1e-5, rtol=1e-6)

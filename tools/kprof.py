@@ -22,6 +22,7 @@ SITES += [("corr_bwd", (DB, C, H, W, True, True)) for C, H, W in KITTI]
 SITES += [("corr_bwd", (DB, C, H, W, n1, not n1)) for C, H, W in KITTI[3:] for n1 in (True, False)]
 SITES += [("corr_bwd_leaky", (DB, C, H, W, True, True)) for C, H, W in KITTI]
 SITES += [("warp_fwd", (DB, C, H, W, "border")) for C, H, W in KITTI[1:]]
+SITES += [("warp_fwd_up", (DB, C, H, W, "border")) for C, H, W in KITTI[1:]]
 SITES += [("warp_bwd", (DB, C, H, W, "border", True, True)) for C, H, W in KITTI[1:]]
 SITES += [("warp_fwd", (8, 3, 256, 832, "border")), ("warp_bwd", (8, 3, 256, 832, "border", False, True))]
 SITES += [("convex_up", (DB, H, W, 4)) for _, H, W in KITTI]

@@ -119,6 +119,8 @@ def main():
             alg = 4 * B * H * W * (4 + 20 * f * f)
         elif op == "warp_fwd":
             alg = warp_bytes(*key[:4])
+        elif op == "warp_fwd_up":  # + the [B,2,H/2,W/2] coarse flow read (the upsampled flow written instead of read)
+            alg = warp_bytes(*key[:4]) + 4 * B * 2 * (H // 2) * (W // 2)
         elif op == "warp_bwd":
             alg = warp_bytes(*key[:4], True, key[5], key[6])
         elif op == "area_pyramid":

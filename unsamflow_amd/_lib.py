@@ -53,6 +53,7 @@ _SIGNATURES = {
         [_c_float_p, _c_float_p, ctypes.c_longlong, _c_float_p] + [ctypes.c_int] * 5 + [ctypes.c_void_p],
         ctypes.c_int,
     ),
+    "usf_warp_fwd_up_f32": ([_c_float_p] * 4 + [ctypes.c_int] * 5 + [ctypes.c_void_p], ctypes.c_int),
     "usf_warp_bwd_f32": (
         [_c_float_p, _c_float_p, ctypes.c_longlong, _c_float_p, _c_float_p, _c_float_p]
         + [ctypes.c_int] * 5

@@ -25,7 +25,7 @@ ARCH = os.environ.get("USF_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 SOURCES = ["corr.hip", "warp.hip", "photo.hip", "upsample.hip", "convex.hip", "stream.hip", "capi.cpp"]
-HEADERS = ["usf_common.h", "warp_tap.h"]
+HEADERS = ["usf_common.h", "warp_tap.h", "interp_tap.h"]
 
 # -fno-slp-vectorize: the SLP vectorizer packs the kernels' independent FMAs into
 # v_pk_fma_f32 / v_pk_add_f32, whose operands must sit in aligned register pairs:

@@ -265,6 +265,28 @@ int usf_warp_fwd_f32(const float* x, const float* flow, long long flow_bstride, 
                 (hipStream_t)stream);
 }
 
+int usf_warp_fwd_up_f32(const float* x, const float* coarse_flow, float* up_flow, float* out, int B, int C, int H,
+                        int W, int pad_mode, void* stream) {
+  clear_error();
+  const char* fn = "usf_warp_fwd_up_f32";
+  if (!check_dims(fn, B, C, H, W)) return USF_EINVAL;
+  if (pad_mode != USF_PAD_ZEROS && pad_mode != USF_PAD_BORDER) {
+    set_error("%s: unknown pad_mode %d", fn, pad_mode);
+    return USF_EINVAL;
+  }
+  if ((H & 1) || (W & 1) || H < 2 || W < 2) {
+    set_error("%s: H=%d W=%d must be even (the coarse flow is [B,2,H/2,W/2])", fn, H, W);
+    return USF_EINVAL;
+  }
+  if (!x || !coarse_flow || !up_flow || !out) {
+    set_error("%s: null pointer", fn);
+    return USF_EINVAL;
+  }
+  if (const int pe = pre_check(fn, (hipStream_t)stream)) return pe;
+  return finish(fn, warp_fwd_up_launch(x, coarse_flow, up_flow, out, B, C, H, W, pad_mode, (hipStream_t)stream),
+                (hipStream_t)stream);
+}
+
 static int warp_bwd_common(const char* fn, const float* x, const float* flow, long long flow_bstride,
                            const float* gout, float* gx, float* gflow, void* ws, long long ws_bytes, int B,
                            int C, int H, int W, int pad_mode, void* stream, bool persist = false) {

@@ -20,26 +20,11 @@
 #include <algorithm>
 #include <cmath>
 
+#include "interp_tap.h"
 #include "usf_common.h"
 
 namespace usf {
 namespace {
-
-struct Lin {
-  int i0, i1;
-  float l0, l1;
-};
-
-__device__ __forceinline__ Lin lin_tap(int dst, float scale, int in) {
-#pragma clang fp contract(off)
-  const float src = scale * (float)dst;
-  Lin t;
-  t.i0 = (int)src;  // src >= 0: truncation == floor
-  t.i1 = t.i0 + (t.i0 < in - 1 ? 1 : 0);
-  t.l1 = src - (float)t.i0;
-  t.l0 = 1.f - t.l1;
-  return t;
-}
 
 __global__ __launch_bounds__(256) void upsample_fwd_kernel(const float* __restrict__ x,
                                                            float* __restrict__ out, long long planes,
@@ -53,10 +38,7 @@ __global__ __launch_bounds__(256) void upsample_fwd_kernel(const float* __restri
   const int oy = (int)((i / Wo) % Ho);
   const long long pl = i / ((long long)Ho * Wo);
   const float* xp = x + pl * H * W;
-  const Lin ty = lin_tap(oy, sy, H), tx = lin_tap(ox, sx, W);
-  const float v00 = xp[ty.i0 * W + tx.i0] * k, v01 = xp[ty.i0 * W + tx.i1] * k;
-  const float v10 = xp[ty.i1 * W + tx.i0] * k, v11 = xp[ty.i1 * W + tx.i1] * k;
-  out[i] = ty.l0 * (tx.l0 * v00 + tx.l1 * v01) + ty.l1 * (tx.l0 * v10 + tx.l1 * v11);
+  out[i] = up_bilinear(xp, W, lin_tap(oy, sy, H), lin_tap(ox, sx, W), k);
 }
 
 // total weight output index `o` (tap t) gives input index `in_i` along one axis
@@ -173,10 +155,6 @@ __global__ __launch_bounds__(256) void area_pyramid_kernel(const float* __restri
     reinterpret_cast<float2*>(p2 + r * W2)[0] =
         make_float2(bsum(4 * r, 0, 4) / 4.f / 4.f, bsum(4 * r, 4, 4) / 4.f / 4.f);
   o3[pl * (H >> 3) * W3 + by * W3 + bx] = bsum(0, 0, 8) / 8.f / 8.f;
-}
-
-inline float ac_scale(int in, int out) {
-  return out > 1 ? (float)(in - 1) / (float)(out - 1) : 0.f;
 }
 
 }  // namespace

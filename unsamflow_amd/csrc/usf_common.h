@@ -95,6 +95,11 @@ long long corr_fwd_workspace(int B, int C, int H, int W, int d);
 hipError_t corr_bwd_launch(const float* x1, const float* x2, const float* gout,
                            float* gx1, float* gx2, int B, int C, int H, int W, int d,
                            hipStream_t s, BwdEpi ep);
+// the decoder's x2 flow upsampling fused into the warp forward: up = [B,2,H,W]
+// = F.interpolate(coarse * 2, scale_factor=2, bilinear, align_corners=True)
+// of coarse = [B,2,H/2,W/2] (H, W even), out = flow_warp(x, up)
+hipError_t warp_fwd_up_launch(const float* x, const float* coarse, float* up, float* out, int B, int C, int H, int W,
+                              int pad_mode, hipStream_t s);
 hipError_t warp_fwd_launch(const float* x, const float* flow, long long flow_bstride,
                            float* out, int B, int C, int H, int W, int pad_mode,
                            hipStream_t s);

@@ -25,6 +25,7 @@
 #include <algorithm>
 #include <climits>
 
+#include "interp_tap.h"
 #include "usf_common.h"
 #include "warp_tap.h"
 
@@ -95,11 +96,22 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t sample_rsrc(const float* p, in
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), 0, bytes, 0x00020000);
 }
 
-template <bool BORDER, int CS>
+// UP: the flow is the decoder's x2 upsampling of a coarse [B,2,H/2,W/2] flow
+// (pwclite.py:299-302: flow = F.interpolate(flow * 2, ...), then
+// flow_warp(x2, flow)), formed per pixel as upsample_fwd_kernel forms it
+// (interp_tap.h: the same numbers) and written once to `up` ([B,2,H,W], by the
+// first channel slice) beside the warp: one launch instead of two.
+struct UpArgs {
+  const float* coarse = nullptr;  // [B,2,h,w] dense
+  float* up = nullptr;            // [B,2,H,W] dense
+  int h = 0, w = 0;
+  float sy = 0.f, sx = 0.f;       // ac_scale(h, H), ac_scale(w, W)
+};
+template <bool BORDER, int CS, bool UP = false>
 __global__ __launch_bounds__(256) void warp_fwd_kernel(const float* __restrict__ x,
                                                        const float* __restrict__ flow,
                                                        long long fbs, float* __restrict__ out,
-                                                       int B, int C, int H, int W) {
+                                                       int B, int C, int H, int W, UpArgs ua = {}) {
   constexpr int PXB = 256 / CS;
   const int HW = H * W;
   const int t = threadIdx.x;
@@ -109,8 +121,22 @@ __global__ __launch_bounds__(256) void warp_fwd_kernel(const float* __restrict__
   const int p = bx * PXB + (t - slice * PXB);
   if (p >= HW) return;
   const int y = p / W, xx = p - y * W;
-  const float* fb = flow + b * fbs;
-  const Tap tp = make_tap(fb[p], fb[HW + p], xx, y, H, W, BORDER);
+  float u, v;
+  if constexpr (UP) {
+    const Lin ty = lin_tap(y, ua.sy, ua.h), tx = lin_tap(xx, ua.sx, ua.w);
+    const float* cb = ua.coarse + (size_t)b * 2 * ua.h * ua.w;
+    u = up_bilinear(cb, ua.w, ty, tx, 2.f);
+    v = up_bilinear(cb + ua.h * ua.w, ua.w, ty, tx, 2.f);
+    if (slice == 0) {
+      ua.up[(size_t)b * 2 * HW + p] = u;
+      ua.up[(size_t)b * 2 * HW + HW + p] = v;
+    }
+  } else {
+    const float* fb = flow + b * fbs;
+    u = fb[p];
+    v = fb[HW + p];
+  }
+  const Tap tp = make_tap(u, v, xx, y, H, W, BORDER);
   const float wnw = tp.s * tp.e, wne = tp.s * tp.w, wsw = tp.n * tp.e, wse = tp.n * tp.w;
   float* ob = out + (size_t)b * C * HW + p;
   if (USF_WARP_FWD_PAIR && W >= 2) {  // corner pairs (pair_tap)
@@ -848,22 +874,22 @@ inline int pick_cs(int B, int C, int HW) {
   return 64;
 }
 
-template <bool BORDER, int CS>
+template <bool BORDER, int CS, bool UP>
 void fwd_launch_cs(const float* x, const float* flow, long long fbs, float* out, int B, int C,
-                   int H, int W, hipStream_t s) {
+                   int H, int W, hipStream_t s, const UpArgs& ua) {
   const dim3 grid((unsigned)((H * W + 256 / CS - 1) / (256 / CS)), (unsigned)B), block(256);
-  hipLaunchKernelGGL((warp_fwd_kernel<BORDER, CS>), grid, block, 0, s, x, flow, fbs, out, B, C, H,
-                     W);
+  hipLaunchKernelGGL((warp_fwd_kernel<BORDER, CS, UP>), grid, block, 0, s, x, flow, fbs, out, B, C, H,
+                     W, ua);
 }
 
-template <bool BORDER>
+template <bool BORDER, bool UP = false>
 void fwd_launch_pad(const float* x, const float* flow, long long fbs, float* out, int B, int C,
-                    int H, int W, hipStream_t s) {
+                    int H, int W, hipStream_t s, const UpArgs& ua = {}) {
   switch (pick_cs(B, C, H * W)) {
-    case 1: fwd_launch_cs<BORDER, 1>(x, flow, fbs, out, B, C, H, W, s); break;
-    case 4: fwd_launch_cs<BORDER, 4>(x, flow, fbs, out, B, C, H, W, s); break;
-    case 16: fwd_launch_cs<BORDER, 16>(x, flow, fbs, out, B, C, H, W, s); break;
-    default: fwd_launch_cs<BORDER, 64>(x, flow, fbs, out, B, C, H, W, s); break;
+    case 1: fwd_launch_cs<BORDER, 1, UP>(x, flow, fbs, out, B, C, H, W, s, ua); break;
+    case 4: fwd_launch_cs<BORDER, 4, UP>(x, flow, fbs, out, B, C, H, W, s, ua); break;
+    case 16: fwd_launch_cs<BORDER, 16, UP>(x, flow, fbs, out, B, C, H, W, s, ua); break;
+    default: fwd_launch_cs<BORDER, 64, UP>(x, flow, fbs, out, B, C, H, W, s, ua); break;
   }
 }
 
@@ -1366,6 +1392,22 @@ hipError_t warp_fwd_launch(const float* x, const float* flow, long long fbs, flo
     fwd_launch_pad<true>(x, flow, fbs, out, B, C, H, W, s);
   else
     fwd_launch_pad<false>(x, flow, fbs, out, B, C, H, W, s);
+  return hipGetLastError();
+}
+
+hipError_t warp_fwd_up_launch(const float* x, const float* coarse, float* up, float* out, int B, int C, int H, int W,
+                              int pad_mode, hipStream_t s) {
+  UpArgs ua;
+  ua.coarse = coarse;
+  ua.up = up;
+  ua.h = H / 2;
+  ua.w = W / 2;
+  ua.sy = ac_scale(ua.h, H);
+  ua.sx = ac_scale(ua.w, W);
+  if (pad_mode == 1)
+    fwd_launch_pad<true, true>(x, nullptr, 0, out, B, C, H, W, s, ua);
+  else
+    fwd_launch_pad<false, true>(x, nullptr, 0, out, B, C, H, W, s, ua);
   return hipGetLastError();
 }
 

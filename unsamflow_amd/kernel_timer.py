@@ -267,6 +267,9 @@ def site_launcher(op: str, key, device, seed: int = 0):
     flow = (torch.sin(2 * xx + ph) + torch.cos(3 * yy - ph)).contiguous()  # [B,2,H,W], |f| <= 2
     if op == "warp_fwd":
         return lambda: ops.warp_forward(x, flow, pad)
+    if op == "warp_fwd_up":  # the decoder's x2 upsampling of a coarse flow fused with the warp
+        coarse = (flow[:, :, ::2, ::2] * 0.5).contiguous()
+        return lambda: ops.warp_forward_up(x, coarse, pad)
     need_x, need_flow = key[5], key[6]
     go = torch.randn(B, C, H, W, device=device, generator=g)
     return lambda: ops.warp_backward(x, flow, go, pad, need_x, need_flow)

@@ -701,6 +701,31 @@ def flow_upsample(flow: torch.Tensor, factor: int) -> torch.Tensor:
     return out
 
 
+def warp_forward_up(x: torch.Tensor, coarse_flow: torch.Tensor, pad: str = "border") -> tuple[torch.Tensor, torch.Tensor]:
+    """(up, out): up = F.interpolate(coarse_flow * 2, scale_factor=2, bilinear,
+    align_corners=True) and out = flow_warp(x, up) (pwclite.py:299-302) in ONE
+    launch (``usf_warp_fwd_up_f32``); the same numbers as :func:`flow_upsample`
+    followed by :func:`warp_forward`."""
+    _require_device_f32("x", x)
+    _require_device_f32("coarse_flow", coarse_flow)
+    B, C, H, W = _nchw("x", x)
+    if pad not in PAD_MODES:
+        raise NotImplementedError(f"flow_warp padding mode {pad!r} (supported: border, zeros)")
+    if tuple(coarse_flow.shape) != (B, 2, H // 2, W // 2) or H % 2 or W % 2:
+        raise ValueError(f"coarse flow shape {tuple(coarse_flow.shape)} is not [B,2,H/2,W/2] of x {(B, C, H, W)}")
+    xc, fc = x.contiguous(), coarse_flow.contiguous()
+    up = torch.empty((B, 2, H, W), device=x.device, dtype=torch.float32)
+    out = torch.empty_like(xc)
+    lib = _lib.load()
+    _args = (xc.data_ptr(), fc.data_ptr(), up.data_ptr(), out.data_ptr(), B, C, H, W, PAD_MODES[pad],
+             _lib.stream_handle(x.device),)
+    with torch.cuda.device(x.device), _kt.timed("warp_fwd_up", (B, C, H, W, pad), x.device,
+                                                  _kt.warp_bytes(B, C, H, W) + 4 * B * 2 * (H // 2) * (W // 2)):
+        rc = lib.usf_warp_fwd_up_f32(*_args)
+    _lib.check(rc, "usf_warp_fwd_up_f32")
+    return up, out
+
+
 def flow_upsample_backward(grad_out: torch.Tensor, factor: int) -> torch.Tensor:
     _require_device_f32("grad_out", grad_out)
     B, C, Ho, Wo = _nchw("grad_out", grad_out)

@@ -157,6 +157,10 @@ def _default_corr():
     return Correlation(pad_size=4, kernel_size=1, max_displacement=4, stride1=1, stride2=1, corr_multiply=1)
 
 
+# the decoder's x2 flow upsampling and warp of x2 as one launch (upsample.upsample_warp)
+FUSED_UP_WARP = True
+
+
 def _default_warp():
     from .warp_utils import flow_warp
 
@@ -229,12 +233,23 @@ class PWCLite(nn.Module):
             return upsample_flow(flow, k)
         return F.interpolate(flow * k, scale_factor=k, mode="bilinear", align_corners=True)
 
+    def _fused_up_warp(self, flow):
+        """The library's own upsampling and warp on a ROCm device (not an injected warp)."""
+        from .warp_utils import flow_warp
+
+        return FUSED_UP_WARP and self.fused_corr_cat and flow.is_cuda and self.warp is flow_warp
+
     def decoder(self, x1_pyramid, x2_pyramid, full_seg1=None, full_seg2=None):
         flows, deferred = [], []
         B, _, h0, w0 = x1_pyramid[0].size()
         flow = torch.zeros(B, 2, h0, w0, dtype=x1_pyramid[0].dtype, device=x1_pyramid[0].device).float()
         for level, (x1, x2) in enumerate(zip(x1_pyramid, x2_pyramid)):
-            if level > 0:
+            if level > 0 and self._fused_up_warp(flow):
+                # x2 upsampling and the warp of x2 in one launch (the same numbers)
+                from .upsample import upsample_warp
+
+                flow, x2_warp = upsample_warp(flow, x2)
+            elif level > 0:
                 flow = self._upsample(flow, 2)
                 x2_warp = self.warp(x2, flow)
             else:

@@ -5,6 +5,8 @@
   levels, k = 2; the x4 output flows without the learned upsampler) as one HIP
   op per direction (csrc/upsample.hip): the scale is folded into the taps and
   the backward is a deterministic gather instead of ATen's atomic scatter.
+* ``upsample_warp``: that x2 upsampling fused with the decoder's warp of x2 at
+  the upsampled flow (pwclite.py:299-302), one forward launch for both.
 * ``convex_upsample``: the learned RAFT-style upsampler of the output flows,
   ``UpFlowNetwork.upsample_flow(flow, 0.25 * convs(feat))`` (pwclite.py:
   140-166; on in kitti_base / sintel_base), as one HIP pass forward and a
@@ -79,6 +81,41 @@ def convex_upsample_pyramid(flows, masks, factor: int = 4, mask_scale: float = 0
     """``[convex_upsample(f, m, factor, mask_scale) for f, m in zip(flows, masks)]``
     in one launch forward and one (+ one gather) backward."""
     return list(ConvexUpsamplePyramidFunction.apply(int(factor), float(mask_scale), len(flows), *flows, *masks))
+
+
+class UpsampleWarpFunction(Function):
+    """The decoder's ``flow = upsample_flow(coarse, 2); x2_warp = flow_warp(x2, flow)``
+    (pwclite.py:299-302) with ONE forward launch (``ops.warp_forward_up``: the
+    same numbers). Backward: the warp backward at the upsampled flow, its flow
+    gradient added to the one the upsampled flow receives from its other uses,
+    then the upsampling backward -- what autograd does for the two-op form."""
+
+    @staticmethod
+    def forward(ctx, coarse, x, pad):
+        up, out = ops.warp_forward_up(x, coarse, pad)
+        ctx.pad = pad
+        ctx.save_for_backward(x, up)
+        return up, out
+
+    @staticmethod
+    def backward(ctx, g_up, g_out):
+        x, up = ctx.saved_tensors
+        need_c, need_x = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+        gx = gflow = None
+        if g_out is not None and (need_x or need_c):
+            gx, gflow = ops.warp_backward(x, up, g_out, ctx.pad, need_x=need_x, need_flow=need_c)
+        gc = None
+        if need_c:
+            g = gflow if g_up is None else (g_up if gflow is None else g_up + gflow)
+            if g is not None:
+                gc = ops.flow_upsample_backward(g, 2)
+        return gc, gx, None
+
+
+def upsample_warp(coarse: torch.Tensor, x: torch.Tensor, pad: str = "border"):
+    """``(up, flow_warp(x, up))`` with ``up = F.interpolate(coarse * 2, scale_factor=2,
+    mode="bilinear", align_corners=True)`` (pwclite.py:299-302), one launch forward."""
+    return UpsampleWarpFunction.apply(coarse, x, pad)
 
 
 def upsample_flow(flow: torch.Tensor, factor: int) -> torch.Tensor:
