@@ -350,6 +350,13 @@ int usf_flow_upsample_f32(const float* flow, float* out, int B, int C, int H, in
 int usf_flow_upsample_bwd_f32(const float* grad_out, float* grad_flow, int B, int C, int H,
                               int W, int factor, void* stream);
 
+/* The same backward of grad_a + grad_b (summed per element in the kernel: the
+ * same numbers as an add followed by usf_flow_upsample_bwd_f32; ABI 8) -- the
+ * decoder's upsampled flow receives one gradient from the warp and one from
+ * its other uses (usf_warp_fwd_up_f32's backward). */
+int usf_flow_upsample_bwd_sum_f32(const float* grad_a, const float* grad_b, float* grad_flow, int B, int C, int H,
+                                  int W, int factor, void* stream);
+
 /* The learned (convex) x`factor` upsampler of the output flows
  * (UpFlowNetwork, pwclite.py:148-166; RAFT-style), factor in {2, 4, 8}
  * (the reference uses 4):

@@ -40,7 +40,7 @@ def test_header_declares_the_abi():
          "usf_photo_loss_partials", "usf_photo_loss_fwd_f32", "usf_photo_loss_pair_fwd_f32",
          "usf_photo_loss_bwd_f32", "usf_photo_loss_pyramid_partials", "usf_photo_loss_pyramid_fwd_f32",
          "usf_photo_loss_pyramid_bwd_f32",
-         "usf_flow_upsample_f32", "usf_flow_upsample_bwd_f32", "usf_area_pyramid_f32",
+         "usf_flow_upsample_f32", "usf_flow_upsample_bwd_f32", "usf_flow_upsample_bwd_sum_f32", "usf_area_pyramid_f32",
          "usf_convex_upsample_f32", "usf_convex_upsample_bwd_scratch", "usf_convex_upsample_bwd_f32",
          "usf_convex_upsample_pyramid_f32", "usf_convex_upsample_pyramid_bwd_scratch",
          "usf_convex_upsample_pyramid_bwd_f32",
@@ -108,6 +108,7 @@ def test_no_torch_types_in_abi():
         (lambda L: L.usf_corr_bwd_ex_f32(1, 1, 1, 81 * 20, 1, None, 0.1, None, 1, 1, 2, 4, 4, 5, 4, None), "scratch"),
         (lambda L: L.usf_flow_upsample_f32(1, 1, 1, 2, 4, 4, 0, None), "bad factor"),
         (lambda L: L.usf_flow_upsample_bwd_f32(None, 1, 1, 2, 4, 4, 2, None), "null pointer"),
+        (lambda L: L.usf_flow_upsample_bwd_sum_f32(1, None, 1, 1, 2, 4, 4, 2, None), "null pointer"),
         (lambda L: L.usf_splat_map_f32(1, 2 * 16, 1, 0, 4, 4, 0, None), "non-positive"),
         (lambda L: L.usf_splat_map_f32(None, 2 * 16, 1, 1, 4, 4, 0, None), "null pointer"),
         (lambda L: L.usf_occ_backward_f32(1, 3, 1, 2, 4, 4, 0.2, None), "batch stride"),

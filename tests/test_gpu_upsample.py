@@ -167,3 +167,15 @@ def test_upsample_warp_equals_separate_calls(hip_device, B, C, H, W, pad):
     # add their excess with fp32 atomics, so two calls agree to rounding only
     torch.testing.assert_close(x2.grad, x1.grad, atol=1e-5, rtol=1e-5)
     torch.testing.assert_close(c2.grad, c1.grad, atol=1e-5, rtol=1e-6)
+
+
+@pytest.mark.parametrize("shape", [(16, 2, 8, 26), (16, 2, 64, 208), (3, 2, 5, 7)])
+def test_upsample_backward_of_a_sum_is_bit_exact(hip_device, shape):
+    """usf_flow_upsample_bwd_sum_f32(a, b) == usf_flow_upsample_bwd_f32(a + b):
+    the per-element add inside the gather is the same IEEE add."""
+    from unsamflow_amd import ops
+
+    B, C, h, w = shape
+    a = torch.from_numpy(hashrng.normal((B, C, 2 * h, 2 * w), 440)).to(hip_device)
+    b = torch.from_numpy(hashrng.normal((B, C, 2 * h, 2 * w), 441)).to(hip_device)
+    assert torch.equal(ops.flow_upsample_backward(a, 2, b), ops.flow_upsample_backward(a + b, 2))

@@ -54,6 +54,7 @@ _SIGNATURES = {
         ctypes.c_int,
     ),
     "usf_warp_fwd_up_f32": ([_c_float_p] * 4 + [ctypes.c_int] * 5 + [ctypes.c_void_p], ctypes.c_int),
+    "usf_flow_upsample_bwd_sum_f32": ([_c_float_p] * 3 + [ctypes.c_int] * 5 + [ctypes.c_void_p], ctypes.c_int),
     "usf_warp_bwd_f32": (
         [_c_float_p, _c_float_p, ctypes.c_longlong, _c_float_p, _c_float_p, _c_float_p]
         + [ctypes.c_int] * 5

@@ -653,6 +653,24 @@ int usf_flow_upsample_bwd_f32(const float* grad_out, float* grad_flow, int B, in
                 (hipStream_t)stream);
 }
 
+int usf_flow_upsample_bwd_sum_f32(const float* grad_a, const float* grad_b, float* grad_flow, int B, int C, int H,
+                                  int W, int factor, void* stream) {
+  clear_error();
+  const char* fn = "usf_flow_upsample_bwd_sum_f32";
+  if (!check_dims(fn, B, C, H, W)) return USF_EINVAL;
+  if (factor < 1 || factor > 16 || (long long)C * H * W * factor * factor > 0x1FFFFFFBLL) {
+    set_error("%s: bad factor %d", fn, factor);
+    return USF_EINVAL;
+  }
+  if (!grad_a || !grad_b || !grad_flow) {
+    set_error("%s: null pointer", fn);
+    return USF_EINVAL;
+  }
+  if (const int pe = pre_check(fn, (hipStream_t)stream)) return pe;
+  return finish(fn, upsample_bwd_launch(grad_a, grad_flow, B, C, H, W, factor, (hipStream_t)stream, grad_b),
+                (hipStream_t)stream);
+}
+
 static bool check_convex(const char* fn, int B, int H, int W, int factor) {
   if (!check_dims(fn, B, 2, H, W)) return false;
   if (!convex_factor_ok(factor)) {

@@ -60,11 +60,15 @@ __device__ __forceinline__ void tap_window(int i, float s, int out, int& o0, int
 // the weights are computed once per axis and all loads are issued
 // unconditionally at clamped offsets (zero weights outside the window: adding
 // 0 * g leaves the sums unchanged). NWIN == 0: the generic loop.
-template <int NWIN>
+// TWO: the output gradient is gout + gout2 (the decoder's upsampled flow gets
+// one gradient from the warp and one from its other uses; summed here per
+// element, the same number as a separate add)
+template <int NWIN, bool TWO = false>
 __global__ __launch_bounds__(256) void upsample_bwd_kernel(const float* __restrict__ gout,
                                                            float* __restrict__ gx, long long planes,
                                                            int H, int W, int Ho, int Wo, float sy,
-                                                           float sx, float k) {
+                                                           float sx, float k,
+                                                           const float* __restrict__ gout2 = nullptr) {
 #pragma clang fp contract(off)
   const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
   const long long n = planes * H * W;
@@ -73,6 +77,8 @@ __global__ __launch_bounds__(256) void upsample_bwd_kernel(const float* __restri
   const int iy = (int)((i / W) % H);
   const long long pl = i / ((long long)H * W);
   const float* gp = gout + pl * Ho * Wo;
+  const float* gp2 = TWO ? gout2 + pl * Ho * Wo : gp;
+  auto g = [&](int o) { return TWO ? gp[o] + gp2[o] : gp[o]; };
   int oy0, oy1, ox0, ox1;
   tap_window(iy, sy, Ho, oy0, oy1);
   tap_window(ix, sx, Wo, ox0, ox1);
@@ -90,10 +96,10 @@ __global__ __launch_bounds__(256) void upsample_bwd_kernel(const float* __restri
     for (int r = 0; r < NWIN; ++r) {
       const int oy = oy0 + r;
       const float wy = oy <= oy1 ? axis_weight(lin_tap(oy, sy, H), iy) : 0.f;
-      const float* row_p = gp + min(oy, Ho - 1) * Wo;
+      const int ro = min(oy, Ho - 1) * Wo;
       float row = 0.f;
 #pragma unroll
-      for (int j = 0; j < NWIN; ++j) row += wx[j] * row_p[cx[j]];
+      for (int j = 0; j < NWIN; ++j) row += wx[j] * g(ro + cx[j]);
       acc += wy * row;
     }
   } else {
@@ -103,7 +109,7 @@ __global__ __launch_bounds__(256) void upsample_bwd_kernel(const float* __restri
       float row = 0.f;
       for (int ox = ox0; ox <= ox1; ++ox) {
         const float wx = axis_weight(lin_tap(ox, sx, W), ix);
-        if (wx != 0.f) row += wx * gp[oy * Wo + ox];
+        if (wx != 0.f) row += wx * g(oy * Wo + ox);
       }
       acc += wy * row;
     }
@@ -183,19 +189,25 @@ static int max_window(int in, int out) {
 }
 
 hipError_t upsample_bwd_launch(const float* gout, float* gx, int B, int C, int H, int W, int k,
-                               hipStream_t s) {
+                               hipStream_t s, const float* gout2) {
   const int Ho = H * k, Wo = W * k;
   const long long planes = (long long)B * C;
   const long long n = planes * H * W;
   const dim3 grid((unsigned)((n + 255) / 256));
   const float sy = ac_scale(H, Ho), sx = ac_scale(W, Wo);
   const int win = std::max(max_window(H, Ho), max_window(W, Wo));
-  if (win <= 8)
-    hipLaunchKernelGGL(upsample_bwd_kernel<8>, grid, dim3(256), 0, s, gout, gx, planes, H, W, Ho, Wo, sy,
-                       sx, (float)k);
+  if (win <= 8 && gout2)
+    hipLaunchKernelGGL((upsample_bwd_kernel<8, true>), grid, dim3(256), 0, s, gout, gx, planes, H, W, Ho, Wo, sy,
+                       sx, (float)k, gout2);
+  else if (win <= 8)
+    hipLaunchKernelGGL((upsample_bwd_kernel<8, false>), grid, dim3(256), 0, s, gout, gx, planes, H, W, Ho, Wo, sy,
+                       sx, (float)k, nullptr);
+  else if (gout2)
+    hipLaunchKernelGGL((upsample_bwd_kernel<0, true>), grid, dim3(256), 0, s, gout, gx, planes, H, W, Ho, Wo, sy,
+                       sx, (float)k, gout2);
   else
-    hipLaunchKernelGGL(upsample_bwd_kernel<0>, grid, dim3(256), 0, s, gout, gx, planes, H, W, Ho, Wo, sy,
-                       sx, (float)k);
+    hipLaunchKernelGGL((upsample_bwd_kernel<0, false>), grid, dim3(256), 0, s, gout, gx, planes, H, W, Ho, Wo, sy,
+                       sx, (float)k, nullptr);
   return hipGetLastError();
 }
 

@@ -152,7 +152,7 @@ hipError_t photo_bwd_launch(const float* basis, const float* coef, const float* 
 hipError_t upsample_fwd_launch(const float* x, float* out, int B, int C, int H, int W, int k,
                                hipStream_t s);
 hipError_t upsample_bwd_launch(const float* gout, float* gx, int B, int C, int H, int W, int k,
-                               hipStream_t s);
+                               hipStream_t s, const float* gout2 = nullptr);
 int convex_pyramid_max_levels();
 hipError_t convex_pyr_fwd_launch(int n, const float* const* flow, const float* const* mask, float* const* out,
                                  const int* H, const int* W, int B, int factor, float mask_scale, hipStream_t s);

@@ -726,7 +726,9 @@ def warp_forward_up(x: torch.Tensor, coarse_flow: torch.Tensor, pad: str = "bord
     return up, out
 
 
-def flow_upsample_backward(grad_out: torch.Tensor, factor: int) -> torch.Tensor:
+def flow_upsample_backward(grad_out: torch.Tensor, factor: int, grad_out2: torch.Tensor | None = None) -> torch.Tensor:
+    """Backward of :func:`flow_upsample` for grad_out (+ grad_out2, summed per
+    element inside the kernel: ``usf_flow_upsample_bwd_sum_f32``)."""
     _require_device_f32("grad_out", grad_out)
     B, C, Ho, Wo = _nchw("grad_out", grad_out)
     k = int(factor)
@@ -736,6 +738,17 @@ def flow_upsample_backward(grad_out: torch.Tensor, factor: int) -> torch.Tensor:
     gc = grad_out.contiguous()
     gx = torch.empty((B, C, H, W), device=grad_out.device, dtype=torch.float32)
     lib = _lib.load()
+    if grad_out2 is not None:
+        _require_device_f32("grad_out2", grad_out2)
+        if grad_out2.shape != grad_out.shape:
+            raise ValueError(f"grad_out2 shape {tuple(grad_out2.shape)} != {tuple(grad_out.shape)}")
+        g2 = grad_out2.contiguous()
+        _args = (gc.data_ptr(), g2.data_ptr(), gx.data_ptr(), B, C, H, W, k, _lib.stream_handle(grad_out.device),)
+        with torch.cuda.device(grad_out.device), _kt.timed("upsample_bwd", (B, C, H, W, k), grad_out.device,
+                                                             4 * B * C * H * W * (1 + 2 * k * k)):
+            rc = lib.usf_flow_upsample_bwd_sum_f32(*_args)
+        _lib.check(rc, "usf_flow_upsample_bwd_sum_f32")
+        return gx
     _args = (gc.data_ptr(), gx.data_ptr(), B, C, H, W, k, _lib.stream_handle(grad_out.device),)
     with torch.cuda.device(grad_out.device), _kt.timed("upsample_bwd", (B, C, H, W, k), grad_out.device,
                                                          4 * B * C * H * W * (1 + k * k)):

@@ -106,9 +106,10 @@ class UpsampleWarpFunction(Function):
             gx, gflow = ops.warp_backward(x, up, g_out, ctx.pad, need_x=need_x, need_flow=need_c)
         gc = None
         if need_c:
-            g = gflow if g_up is None else (g_up if gflow is None else g_up + gflow)
-            if g is not None:
-                gc = ops.flow_upsample_backward(g, 2)
+            if g_up is not None and gflow is not None:  # the add inside the upsampling backward
+                gc = ops.flow_upsample_backward(g_up, 2, gflow)
+            elif g_up is not None or gflow is not None:
+                gc = ops.flow_upsample_backward(g_up if g_up is not None else gflow, 2)
         return gc, gx, None
 
 
