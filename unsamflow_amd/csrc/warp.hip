@@ -383,14 +383,13 @@ struct BinArgs {
   int tiles_x = 0, ntiles = 0; // the gather's 32 x 8 target tiles
 };
 
-template <bool BORDER, bool WANT_GX, bool WANT_GF, int CS, int BIN = 0>
-__global__ __launch_bounds__(256) void warp_bwd_kernel(const float* __restrict__ x,
-                                                       const float* __restrict__ flow,
-                                                       long long fbs,
-                                                       const float* __restrict__ gout,
-                                                       float* __restrict__ gx,
-                                                       float* __restrict__ gflow, int B, int C,
-                                                       int H, int W, BinArgs ba = {}) {
+// The per-pixel backward of one (pixel block bx, sample b): warp_bwd_kernel's
+// body, also run by the small-level fused kernel (warp_bwd_fused_small_kernel)
+template <bool BORDER, bool WANT_GX, bool WANT_GF, int CS, int BIN>
+__device__ __forceinline__ void warp_bwd_body(const float* __restrict__ x, const float* __restrict__ flow,
+                                              long long fbs, const float* __restrict__ gout,
+                                              float* __restrict__ gx, float* __restrict__ gflow, int B, int C,
+                                              int H, int W, const BinArgs& ba, int bx, int b) {
   constexpr int PXB = 256 / CS;
   __shared__ float red[2][256];
   // BIN >= 2: this call's count-buffer parity, loaded first so its latency
@@ -400,8 +399,6 @@ __global__ __launch_bounds__(256) void warp_bwd_kernel(const float* __restrict__
   const int t = threadIdx.x;
   const int slice = t / PXB;
   const int pl = t - slice * PXB;
-  int bx, b;
-  warp_block(bx, b);
   const int p = bx * PXB + pl;
   bool valid = p < HW;
   float dix = 0.f, diy = 0.f;
@@ -555,6 +552,19 @@ __global__ __launch_bounds__(256) void warp_bwd_kernel(const float* __restrict__
     gf[0] = (ggx / (float)(W - 1)) * 2.0f;
     gf[HW] = (ggy / (float)(H - 1)) * 2.0f;
   }
+}
+
+template <bool BORDER, bool WANT_GX, bool WANT_GF, int CS, int BIN = 0>
+__global__ __launch_bounds__(256) void warp_bwd_kernel(const float* __restrict__ x,
+                                                       const float* __restrict__ flow,
+                                                       long long fbs,
+                                                       const float* __restrict__ gout,
+                                                       float* __restrict__ gx,
+                                                       float* __restrict__ gflow, int B, int C,
+                                                       int H, int W, BinArgs ba = {}) {
+  int bx, b;
+  warp_block(bx, b);
+  warp_bwd_body<BORDER, WANT_GX, WANT_GF, CS, BIN>(x, flow, fbs, gout, gx, gflow, B, C, H, W, ba, bx, b);
 }
 
 // The gather pass of the binned grad_x: thread = target cell q, channels
@@ -786,6 +796,156 @@ __global__ __launch_bounds__(256) void warp_gx_bins_kernel(const float* __restri
   }
 }
 
+// Small levels (H*W <= kSmallPx, (H+1)(W+1) <= kSmallCells: KITTI L1,
+// Sintel L1): the whole backward in ONE launch with no workspace. Workgroups
+// [0, B*GA) each bin their sample's source pixels in LDS -- counts per
+// north-west cell (LDS atomics), an exclusive scan, placement, then every
+// cell's pixels sorted by index -- and gather grad_x for their channel group
+// (every target cell sums its four corner cells' pixels in that fixed order:
+// the binned gather's numbers wherever a cell holds at most kBinSlots pixels,
+// and deterministic beyond, with no overflow atomics). The remaining
+// workgroups run the filing pass's grad_flow (warp_bwd_body, the same channel
+// slices as bin_pass picks, so the same numbers) without the filing.
+// (At 832 pixels -- KITTI L2 -- the per-workgroup binning and the longer gather
+// loop made it slower than the two-launch form: 33.6 vs 22.7 us in the step,
+// while L1 went 19.3 -> 14.7 us; profiles/ab_r06/warp_small_fused.json.)
+constexpr int kSmallPx = 512, kSmallCells = 768, kSmallCH = 8;
+template <bool BORDER>
+__device__ void warp_gx_small(const float* __restrict__ flow, long long fbs, const float* __restrict__ gout,
+                              float* __restrict__ gx, int C, int H, int W, int b, int c0, int c1) {
+  __shared__ float s_w[kSmallPx], s_n[kSmallPx];
+  __shared__ int s_cell[kSmallPx], s_list[kSmallPx];
+  __shared__ unsigned char s_m[kSmallPx];
+  __shared__ int s_start[kSmallCells + 1], s_fill[kSmallCells];
+  __shared__ int s_part[256];
+  const int HW = H * W, W1 = W + 1, E = (H + 1) * W1;
+  const int t = threadIdx.x, lane = t & 63;
+  for (int i = t; i <= E; i += 256) s_start[i] = 0;
+  __syncthreads();
+  // taps of every source pixel of sample b; count per north-west cell
+  const float* fb = flow + (size_t)b * fbs;
+  for (int p = t; p < HW; p += 256) {
+    const int y = p / W, xx = p - y * W;
+    const Tap tp = make_tap(fb[p], fb[HW + p], xx, y, H, W, BORDER);
+    s_w[p] = tp.w;
+    s_n[p] = tp.n;
+    s_m[p] = (unsigned char)((tp.m_nw ? 1 : 0) | (tp.m_ne ? 2 : 0) | (tp.m_sw ? 4 : 0) | (tp.m_se ? 8 : 0));
+    int cell = -1;
+    if (tp.m_nw || tp.m_ne || tp.m_sw || tp.m_se) {  // then xw in [-1, W), yn in [-1, H)
+      cell = (tp.yn + 1) * W1 + tp.xw + 1;
+      atomicAdd(&s_start[cell], 1);
+    }
+    s_cell[p] = cell;
+  }
+  __syncthreads();
+  // exclusive scan of the counts: K consecutive cells per thread, the 256
+  // thread totals scanned by wave 0 (4 per lane)
+  const int K = (E + 255) / 256;
+  const int i0 = min(E, t * K), i1 = min(E, i0 + K);
+  int loc = 0;
+  for (int i = i0; i < i1; ++i) loc += s_start[i];
+  s_part[t] = loc;
+  __syncthreads();
+  if (t < 64) {
+    const int a0 = s_part[4 * t], a1 = s_part[4 * t + 1], a2 = s_part[4 * t + 2], a3 = s_part[4 * t + 3];
+    const int sum = a0 + a1 + a2 + a3;
+    int inc = sum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int v = __shfl_up(inc, o);
+      if (lane >= o) inc += v;
+    }
+    const int ex = inc - sum;
+    s_part[4 * t] = ex;
+    s_part[4 * t + 1] = ex + a0;
+    s_part[4 * t + 2] = ex + a0 + a1;
+    s_part[4 * t + 3] = ex + a0 + a1 + a2;
+  }
+  __syncthreads();
+  int run = s_part[t];
+  for (int i = i0; i < i1; ++i) {
+    const int c = s_start[i];
+    s_start[i] = run;
+    s_fill[i] = run;
+    run += c;
+  }
+  if (i0 < i1 && i1 == E) s_start[E] = run;  // the thread holding the last cell
+  __syncthreads();
+  for (int p = t; p < HW; p += 256) {
+    const int cell = s_cell[p];
+    if (cell >= 0) s_list[atomicAdd(&s_fill[cell], 1)] = p;
+  }
+  __syncthreads();
+  // each cell's pixels in index order (placement order is the atomics')
+  for (int c = t; c < E; c += 256) {
+    const int a = s_start[c], z = s_start[c + 1];
+    for (int i = a + 1; i < z; ++i) {
+      const int v = s_list[i];
+      int j = i - 1;
+      while (j >= a && s_list[j] > v) {
+        s_list[j + 1] = s_list[j];
+        --j;
+      }
+      s_list[j + 1] = v;
+    }
+  }
+  __syncthreads();
+  const float* gb = gout + (size_t)b * C * HW;
+  float* gxb = gx + (size_t)b * C * HW;
+  for (int q = t; q < HW; q += 256) {
+    const int qy = q / W, qx = q - qy * W;
+    for (int c = c0; c < c1; c += kSmallCH) {
+      float acc[kSmallCH];
+#pragma unroll
+      for (int u = 0; u < kSmallCH; ++u) acc[u] = 0.f;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int cell = (qy - (k >> 1) + 1) * W1 + (qx - (k & 1) + 1);
+        const int a = s_start[cell], z = s_start[cell + 1];
+        for (int i = a; i < z; ++i) {
+          const int p = s_list[i];
+          const int m = s_m[p];
+          const float w = s_w[p], n = s_n[p];
+          const float e = 1.0f - w, sn = 1.0f - n;  // as make_tap forms them
+          // corner k's weight as the filing pass writes it (BinArgs::wbin)
+          const float wt = k == 0 ? ((m & 1) ? sn * e : 0.f)
+                           : k == 1 ? ((m & 2) ? sn * w : 0.f)
+                           : k == 2 ? ((m & 4) ? n * e : 0.f)
+                                    : ((m & 8) ? n * w : 0.f);
+          const float* src = gb + p;
+#pragma unroll
+          for (int u = 0; u < kSmallCH; ++u)
+            acc[u] = fmaf(wt, src[(size_t)min(c + u, c1 - 1) * HW], acc[u]);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < kSmallCH; ++u)
+        if (c + u < c1) gxb[(size_t)(c + u) * HW + q] = acc[u];
+    }
+  }
+}
+
+template <bool BORDER, int CS, bool WANT_GF>
+__global__ __launch_bounds__(256) void warp_bwd_fused_small_kernel(const float* __restrict__ x,
+                                                                   const float* __restrict__ flow, long long fbs,
+                                                                   const float* __restrict__ gout,
+                                                                   float* __restrict__ gx, float* __restrict__ gflow,
+                                                                   int B, int C, int H, int W, int GA, int cper,
+                                                                   int nbx) {
+  const int i = blockIdx.x;
+  const int nA = B * GA;
+  if (i < nA) {
+    const int b = i / GA, g = i - (i / GA) * GA;
+    warp_gx_small<BORDER>(flow, fbs, gout, gx, C, H, W, b, g * cper, min(C, (g + 1) * cper));
+    return;
+  }
+  if constexpr (WANT_GF) {
+    const int j = i - nA;
+    warp_bwd_body<BORDER, false, true, CS, 0>(x, flow, fbs, gout, nullptr, gflow, B, C, H, W, BinArgs{}, j % nbx,
+                                              j / nbx);
+  }
+}
+
 // Overflow pixels of the binned grad_x add their four corner contributions
 // with float atomics after the gather pass. A wave takes 64 consecutive list
 // entries (lane = entry) x kOvfCh channels: consecutive entries mostly share
@@ -1014,9 +1174,7 @@ inline GatherGrid gather_grid(int B, int C, int H, int W) {
 // smallest slice count in {4, 16, 64} that still gives >= 768 workgroups
 // (profiles/ab_r02/warp_bins_ab.json: L2 31.5 -> 26.7 us with 16 instead of 4;
 // L3/L4 keep 4, L1 64)
-template <bool BORDER, int BINM>
-void bin_pass(const float* x, const float* flow, long long fbs, const float* gout, float* gflow, int B, int C,
-              int H, int W, BinArgs ba, hipStream_t s) {
+inline int bin_cs(int B, int C, int H, int W) {
   int cs = 64;
   for (const int o : {4, 16}) {
     if ((long)B * ((H * W + 256 / o - 1) / (256 / o)) >= 768) {
@@ -1025,6 +1183,13 @@ void bin_pass(const float* x, const float* flow, long long fbs, const float* gou
     }
   }
   while (cs > 4 && cs > C) cs >>= 2;  // no more slices than channels (4 at least)
+  return cs;
+}
+
+template <bool BORDER, int BINM>
+void bin_pass(const float* x, const float* flow, long long fbs, const float* gout, float* gflow, int B, int C,
+              int H, int W, BinArgs ba, hipStream_t s) {
+  int cs = bin_cs(B, C, H, W);
 #ifdef USF_BIN_CS
   cs = USF_BIN_CS;  // A/B builds only
 #endif
@@ -1034,6 +1199,37 @@ void bin_pass(const float* x, const float* flow, long long fbs, const float* gou
     case 16: bin_pass_cs<BORDER, 16, BINM>(x, flow, fbs, gout, gflow, B, C, H, W, ba, s); break;
     default: bin_pass_cs<BORDER, 64, BINM>(x, flow, fbs, gout, gflow, B, C, H, W, ba, s); break;
   }
+}
+
+// The small-level fused backward (warp_bwd_fused_small_kernel): false when the
+// shape is not small enough (or grad_x is not wanted).
+template <bool BORDER, int CS>
+void small_fused_cs(const float* x, const float* flow, long long fbs, const float* gout, float* gx, float* gflow,
+                    int B, int C, int H, int W, hipStream_t s) {
+  const int HW = H * W;
+  const int GA = (C + kSmallCH - 1) / kSmallCH;
+  const int nbx = (HW + 256 / CS - 1) / (256 / CS);
+  const unsigned nblk = (unsigned)(B * GA + (gflow ? B * nbx : 0));
+  if (gflow)
+    hipLaunchKernelGGL((warp_bwd_fused_small_kernel<BORDER, CS, true>), dim3(nblk), dim3(256), 0, s, x, flow, fbs,
+                       gout, gx, gflow, B, C, H, W, GA, kSmallCH, nbx);
+  else
+    hipLaunchKernelGGL((warp_bwd_fused_small_kernel<BORDER, CS, false>), dim3(nblk), dim3(256), 0, s, x, flow, fbs,
+                       gout, gx, gflow, B, C, H, W, GA, kSmallCH, nbx);
+}
+#ifndef USF_WARP_SMALL_FUSED
+#define USF_WARP_SMALL_FUSED 1
+#endif
+template <bool BORDER>
+bool bwd_small_fused(const float* x, const float* flow, long long fbs, const float* gout, float* gx, float* gflow,
+                     int B, int C, int H, int W, hipStream_t s) {
+  if (!USF_WARP_SMALL_FUSED || !gx || H * W > kSmallPx || (long long)(H + 1) * (W + 1) > kSmallCells) return false;
+  switch (bin_cs(B, C, H, W)) {  // grad_flow's slices as the filing pass picks them (the same numbers)
+    case 4: small_fused_cs<BORDER, 4>(x, flow, fbs, gout, gx, gflow, B, C, H, W, s); break;
+    case 16: small_fused_cs<BORDER, 16>(x, flow, fbs, gout, gx, gflow, B, C, H, W, s); break;
+    default: small_fused_cs<BORDER, 64>(x, flow, fbs, gout, gx, gflow, B, C, H, W, s); break;
+  }
+  return true;
 }
 
 // grad_x by the binned gather (+ grad_flow in the filing pass); see BinArgs.
@@ -1156,6 +1352,8 @@ void bwd_launch_pad(const float* x, const float* flow, long long fbs, const floa
                     float* gx, float* gflow, int B, int C, int H, int W, hipStream_t s,
                     void* ws = nullptr, long long ws_bytes = 0, bool persist = false) {
   const int v = variant_override(2);
+  // small levels: one launch, no workspace (the persistent one stays untouched)
+  if ((v < 0 || v == 2) && bwd_small_fused<BORDER>(x, flow, fbs, gout, gx, gflow, B, C, H, W, s)) return;
   if (persist) {  // usf_warp_bwd_persist_f32 (capi.cpp checked the workspace size and C)
     if (gx && (v < 0 || v == 2)) {
       bwd_bins_persist<BORDER>(x, flow, fbs, gout, gx, gflow, B, C, H, W, ws, s);
