@@ -245,8 +245,9 @@ def warp_backward(
     """(grad_x, grad_flow) of :func:`warp_forward`.
 
     grad_x is the library's binned gather in its persistent form
-    (``usf_warp_bwd_persist_f32``, two launches up to 8192 pixels, three above
-    with the overflow pass and no zero fill): every source pixel is filed under its
+    (``usf_warp_bwd_persist_f32``: one launch with LDS binning up to 512 pixels,
+    two launches up to 8192, three above with the overflow pass and no zero
+    fill): every source pixel is filed under its
     north-west corner cell and each target cell sums its sources in a fixed
     order, so grad_x is deterministic unless a cell receives more than 4 source
     pixels (strongly compressive flow), whose excess is added with fp32
